@@ -1,0 +1,105 @@
+"""ctypes front-end of the CPU oracle (oracle/libknn_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package.  See
+knn_oracle.h for what it restates and how it is pinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libknn_oracle.so")
+
+NB_DTYPE = np.dtype([("distance", "<f8"), ("idx", "<i4"), ("label", "<i4")])
+COLMAJOR, ROWMAJOR = 0, 1
+VOTE_SERIAL, VOTE_MPI, VOTE_MAJORITY = 0, 1, 2
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        p, sz, i, d = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double
+        L.orc_knn_rows.argtypes = [p, sz, sz, i, p, sz, sz, i, i, i, p]
+        L.orc_knn_rows.restype = i
+        L.orc_knn_block.argtypes = [p, sz, sz, p, sz, sz, sz, p, i, i, p]
+        L.orc_knn_block.restype = i
+        L.orc_lists_init.argtypes = [p, sz, i]
+        L.orc_lists_init.restype = None
+        L.orc_classify.argtypes = [p, sz, sz, i, i, i, p, p]
+        L.orc_classify.restype = ctypes.c_long
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def knn(X, k=30, labels=None, rows=None, literal=False, nthreads=0, layout="row"):
+    """All-kNN with the reference's serial semantics (serial:57-93).
+
+    X: (m, n) float64 array (row-major in memory unless layout="col", in which
+    case X is the column-major buffer of an (m, n) matrix given as its (n, m)
+    transpose view is NOT assumed: pass a Fortran-ordered array).
+    rows: optional (q0, nq) query range.  Returns a structured array (nq, k).
+    """
+    X = np.asarray(X, dtype=np.float64)
+    m, n = X.shape
+    if layout == "col":
+        buf = np.asfortranarray(X)
+        lay = COLMAJOR
+    else:
+        buf = np.ascontiguousarray(X)
+        lay = ROWMAJOR
+    q0, nq = rows if rows is not None else (0, m)
+    out = np.zeros((nq, k), dtype=NB_DTYPE)
+    lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.float64)
+    rc = lib().orc_knn_rows(_ptr(buf), m, n, lay, _ptr(lab), q0, nq, k,
+                            int(bool(literal)), nthreads, _ptr(out))
+    if rc:
+        raise RuntimeError("orc_knn_rows failed rc=%d" % rc)
+    return out
+
+
+def lists_init(nq, k):
+    out = np.zeros((nq, k), dtype=NB_DTYPE)
+    lib().orc_lists_init(_ptr(out), nq, k)
+    return out
+
+
+def knn_block(Q, q_base, C, c_base, lists, labels=None, nthreads=0):
+    """Fold one corpus block into running lists (ring-step restatement)."""
+    Q = np.ascontiguousarray(Q, dtype=np.float64)
+    C = np.ascontiguousarray(C, dtype=np.float64)
+    assert lists.dtype == NB_DTYPE and lists.flags.c_contiguous
+    nq, n = Q.shape
+    nc = C.shape[0]
+    k = lists.shape[1]
+    lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.float64)
+    rc = lib().orc_knn_block(_ptr(Q), nq, q_base, _ptr(C), nc, c_base, n,
+                             _ptr(lab), k, nthreads, _ptr(lists))
+    if rc:
+        raise RuntimeError("orc_knn_block failed rc=%d" % rc)
+    return lists
+
+
+def classify(nb, labels, nclasses=10, rule=VOTE_SERIAL, q0=0):
+    """Vote + Matches (serial:104-130 / blk:252-270).  Returns (pred, matches)."""
+    nb = np.ascontiguousarray(nb)
+    nq, k = nb.shape
+    lab = np.ascontiguousarray(labels, dtype=np.float64)
+    pred = np.zeros(nq, dtype=np.int32)
+    matches = lib().orc_classify(_ptr(nb), nq, q0, k, nclasses, rule, _ptr(lab), _ptr(pred))
+    return pred, int(matches)
