@@ -1,0 +1,65 @@
+/*
+ * knn_internal.h -- launchers exported by knn_kernels.hip to the host C
+ * engine (knn_engine.c).  Plain C ABI, device pointers, hipStream_t as void*.
+ */
+#ifndef KNN_INTERNAL_H
+#define KNN_INTERNAL_H
+#include <stddef.h>
+#include <stdint.h>
+#include "knn.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Tile geometry shared by host and device. */
+#define KNN_TQ 128        /* queries per workgroup (8 waves x 16)      */
+#define KNN_TC 128        /* corpus rows per tile                      */
+#define KNN_BK 16         /* features per LDS chunk                    */
+#define KNN_KL 16         /* per-lane candidate list capacity          */
+#define KNN_KP 32         /* per-query state / selection capacity      */
+#define KNN_ROW_ALIGN 128 /* packed-block row padding                  */
+
+/* meta doubles of a packed block */
+#define KNN_META_MAXABS    0
+#define KNN_META_MAXNORM   1
+#define KNN_META_NONINT    2
+#define KNN_META_NONFINITE 3
+
+/* engine modes (decided on device from the reduced meta) */
+#define KNN_MODE_INT  0   /* integer data: GEMM-form d^2 is exact         */
+#define KNN_MODE_GEMM 1   /* fp64 GEMM-form filter + exact re-rank        */
+#define KNN_MODE_SCAN 2   /* non-finite / huge data: exact scan only      */
+
+static inline size_t knn_round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+static inline size_t knn_rows_pad(size_t rows) { return knn_round_up(rows ? rows : 1, KNN_ROW_ALIGN); }
+static inline size_t knn_n_pad(size_t n) { return knn_round_up(n ? n : 1, KNN_BK); }
+
+int knn_launch_pack(double *blk, size_t cap, size_t rows, size_t n, const double *src,
+                    size_t ld, int layout, void *stream);
+int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_t q_base, int nq,
+                         const double *cblk, size_t c_rows_pad, size_t c_base, int nc,
+                         int n, const double *meta, int nsplit,
+                         double *part_d, int *part_i, double *part_T, int nq_pad,
+                         void *stream);
+int knn_launch_merge(const double *part_d, const int *part_i, const double *part_T,
+                     int nsplit, int nq, int nq_pad, int first_step,
+                     double *st_d, double *st_x, int *st_i, double *st_T,
+                     const double *qblk, const double *cblk, size_t c_base, int nc,
+                     int n, const double *meta, void *stream);
+int knn_launch_finalize(const double *st_d, const double *st_x, const int *st_i,
+                        const double *st_T, const double *qblk, size_t q_rows_pad,
+                        int nq, int n, int k, const double *meta,
+                        knn_neighbour_t *out, int *fail_count, int *fail_list,
+                        int *mode_out, void *stream);
+int knn_launch_rescan_init(double *rs_d, int *rs_i, int nfail, void *stream);
+int knn_launch_rescan_step(const int *fail_list, int nfail, const double *qblk,
+                           size_t q_base, const double *cblk, size_t c_base, int nc,
+                           int n, double *rs_d, int *rs_i, void *stream);
+int knn_launch_rescan_end(const int *fail_list, int nfail, const double *rs_d,
+                          const int *rs_i, int k, knn_neighbour_t *out, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,734 @@
+// knn_kernels.hip -- CDNA4 (gfx950) kernels of the all-kNN engine.
+//
+// Hot path of yiapou13/mpi-knn: the distance loop + k-smallest insertion of
+// knn-serial.c:72-93 (and its per-block copies mpi-knn-parallel_blocking.c:
+// 155-181, 217-242).  Re-designed for MI355X:
+//
+//   k_pack       column/row-major fp64 -> padded row-major block + norms +
+//                meta (replaces blk:100-109's packing).
+//   k_dist_topk  fused fp64-MFMA contraction G = C.Q^T (v_mfma_f64_16x16x4)
+//                with d^2 = |q|^2 + |c|^2 - 2G and a per-lane register top-k
+//                (insertion network) behind a shared threshold.  One
+//                workgroup = 128 queries x a corpus split; tiles of 128 rows
+//                stream through LDS by global_load_lds, double-buffered.
+//   k_merge      per query: tournament merge of the split/lane lists with
+//                the running state (ring steps), exact re-rank of new
+//                entries in reference order (GEMM mode).
+//   k_finalize   order by (sqrt(S), idx), drop S == 0, certify that no
+//                unseen candidate can enter the top-k, emit records.
+//   k_rescan_*   exact reference-order scan for the (rare) queries the
+//                certificate could not clear.
+//
+// Layout and roofline notes: DESIGN.md sec.4.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "knn_internal.h"
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+#define LDS_AS __attribute__((address_space(3)))
+
+static constexpr double KNN_INF = __builtin_inf();
+
+// ---------------------------------------------------------------------------
+// Mode decision from the max-reduced meta (identical on every rank).
+//   INT : every value an integer and (2 max|x|)^2 n <= 2^51, so every
+//         partial sum of both the reference's sum of squares and of the
+//         GEMM form is an exact integer < 2^51, d^2 is bit-identical to the
+//         reference's S and sqrt is injective on it.
+//   SCAN: non-finite values or norms near overflow -- no error bound.
+//   GEMM: everything else.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int knn_mode(const double *meta, int n)
+{
+    if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e290))
+        return KNN_MODE_SCAN;
+    const double lim = 2251799813685248.0 / (4.0 * (double)n);   // 2^51 / 4n
+    double mx = meta[KNN_META_MAXABS];
+    if (meta[KNN_META_NONINT] == 0.0 && mx * mx <= lim) return KNN_MODE_INT;
+    return KNN_MODE_GEMM;
+}
+
+// Reference-order exact squared distance: S = S + (a-b)^2 over j = 0..n-1,
+// two roundings per feature, no FMA (knn-serial.c:76-85; pow(x,2) -> x*x).
+__device__ __attribute__((noinline)) double knn_exact_sq(const double *__restrict__ a,
+                                                         const double *__restrict__ b, int n)
+{
+#pragma clang fp contract(off)
+    double S = 0.0;
+    for (int j = 0; j < n; j++) {
+        double t = a[j] - b[j];
+        double t2 = t * t;
+        S = S + t2;
+    }
+    return S;
+}
+
+// ---------------------------------------------------------------------------
+// k_pack: src (col-major, ld >= rows | row-major, ld >= n) -> padded row-major
+// block.  64x64 tiles through LDS so both sides stay coalesced.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pack(double *__restrict__ blk, size_t rows,
+                                              size_t rows_pad, int n, int n_pad,
+                                              const double *__restrict__ src, size_t ld,
+                                              int layout)
+{
+    __shared__ double tile[64][65];
+    const size_t i0 = (size_t)blockIdx.x * 64;
+    const int j0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    if (layout == KNN_COLMAJOR) {
+        for (int jj = ty; jj < 64; jj += 4) {
+            size_t i = i0 + tx;
+            int j = j0 + jj;
+            tile[jj][tx] = (i < rows && j < n) ? src[i + (size_t)j * ld] : 0.0;
+        }
+    } else {
+        for (int ii = ty; ii < 64; ii += 4) {
+            size_t i = i0 + ii;
+            int j = j0 + tx;
+            tile[tx][ii] = (i < rows && j < n) ? src[i * ld + j] : 0.0;
+        }
+    }
+    __syncthreads();
+    for (int ii = ty; ii < 64; ii += 4) {
+        size_t i = i0 + ii;
+        int j = j0 + tx;
+        if (i < rows_pad && j < n_pad) blk[i * n_pad + j] = tile[tx][ii];
+    }
+}
+
+// One wave per row: squared norm + meta (max|x|, max norm, non-integer,
+// non-finite).  Block-reduced, then one atomicMax per block and word.
+__global__ __launch_bounds__(256) void k_norms(double *__restrict__ blk, size_t rows,
+                                               size_t rows_pad, int n, int n_pad)
+{
+    double *norms = blk + rows_pad * (size_t)n_pad;
+    double *meta = norms + rows_pad;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double mabs = 0.0, mnorm = 0.0, nonint = 0.0, nonfin = 0.0;
+    for (size_t i = (size_t)blockIdx.x * 4 + wave; i < rows_pad; i += (size_t)gridDim.x * 4) {
+        const double *x = blk + i * n_pad;
+        double s = 0.0;
+        if (i < rows) {
+            for (int j = lane; j < n; j += 64) {
+                double v = x[j];
+                s = fma(v, v, s);
+                if (!__builtin_isfinite(v)) nonfin = 1.0;
+                else {
+                    double a = fabs(v);
+                    mabs = a > mabs ? a : mabs;
+                    if (v != rint(v)) nonint = 1.0;
+                }
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+        if (lane == 0) norms[i] = s;
+        if (s == s) mnorm = s > mnorm ? s : mnorm;
+        else nonfin = 1.0;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        mabs = fmax(mabs, __shfl_xor(mabs, off));
+        mnorm = fmax(mnorm, __shfl_xor(mnorm, off));
+        nonint = fmax(nonint, __shfl_xor(nonint, off));
+        nonfin = fmax(nonfin, __shfl_xor(nonfin, off));
+    }
+    __shared__ double red[4][4];
+    if (lane == 0) {
+        red[wave][0] = mabs; red[wave][1] = mnorm; red[wave][2] = nonint; red[wave][3] = nonfin;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        double v = fmax(fmax(red[0][threadIdx.x], red[1][threadIdx.x]),
+                        fmax(red[2][threadIdx.x], red[3][threadIdx.x]));
+        if (!(v >= 0.0)) v = __builtin_inf();  // NaN norm -> treat as overflow
+        // non-negative doubles order like their bit patterns
+        atomicMax((unsigned long long *)&meta[threadIdx.x],
+                  (unsigned long long)__double_as_longlong(v));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Register top-KP list: L ascending, insertion after equal keys (the lane's
+// candidates arrive in increasing row order, so this is the reference's
+// stable "lower index first" tie rule).  d >= L[KP-1] (incl. +inf,
+// NaN) is a no-op, so lanes without a candidate run it harmlessly.
+// ---------------------------------------------------------------------------
+template <int KP>
+__device__ __forceinline__ void list_insert(double (&L)[KP], int (&I)[KP], double d, int id)
+{
+    bool c_hi = d < L[KP - 1];
+#pragma unroll
+    for (int e = KP - 1; e >= 0; e--) {
+        bool c_lo = (e > 0) ? (d < L[e > 0 ? e - 1 : 0]) : false;
+        double t = c_lo ? L[e > 0 ? e - 1 : 0] : d;
+        int ti = c_lo ? I[e > 0 ? e - 1 : 0] : id;
+        L[e] = c_hi ? t : L[e];
+        I[e] = c_hi ? ti : I[e];
+        c_hi = c_lo;
+    }
+}
+
+__device__ __forceinline__ void wave_argmin(double &d, int &i)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        double od = __shfl_xor(d, off);
+        int oi = __shfl_xor(i, off);
+        bool take = (od < d) || (od == d && oi < i);
+        d = take ? od : d;
+        i = take ? oi : i;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_dist_topk
+//
+// Workgroup: 512 threads = 8 waves; 128 queries (wave w: queries 16w..16w+15)
+// x corpus tiles of 128 rows (8 m-tiles of 16).  Per wave per 16-feature
+// chunk: 8 m-tiles x 4 k-steps = 32 v_mfma_f64_16x16x4_f64.
+//
+// f64 MFMA operand map (probed, tools/probe): lane l supplies A[l&15][l>>4]
+// and B[l>>4][l&15]; D reg r of lane l is D[(l>>4)+4r][l&15].  A = corpus
+// rows, B = queries, so lane l ends with 32 d^2 of ONE query (l&15) against
+// corpus rows 16mt + (l>>4) + 4r.  The 4 lanes sharing a query (l>>4 =
+// 0..3) keep separate lists over disjoint row sets; they share a threshold.
+//
+// k-permutation: in chunk f0, k-step s = 2p+e of lane group g uses feature
+// f0 + 8p + 2g + e, so each lane's two k-steps per piece p are one 16-byte
+// ds_read_b128, and one global_load_lds (1 KiB) stages 16 rows x 64
+// contiguous bytes.  LDS images are lane-linear -> conflict-free reads.
+//
+// LDS (one array, guide 'second __shared__ object' trap):
+//   [0,32K)  C pieces  [buf][mt*2+p][64 lanes][2 doubles]
+//   [32K,64K) Q pieces [buf][w*2+p][64][2]
+//   [64K,66K) corpus norms of the tile, [tile&1][128]
+// ---------------------------------------------------------------------------
+template <int KL, int KS>
+__global__ __launch_bounds__(512, 2) void k_dist_topk(
+    const double *__restrict__ qblk, const double *__restrict__ qnorm, size_t q_base, int nq,
+    const double *__restrict__ cblk, const double *__restrict__ cnorm, size_t c_base, int nc,
+    int n, int n_pad, int ntiles, int nsplit, int nqb, const double *__restrict__ meta,
+    double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T,
+    int nq_pad)
+{
+    __shared__ __attribute__((aligned(16))) char smem[66 * 1024];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane >> 4, j16 = lane & 15;
+    const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;
+    const int t_lo = (int)((long)split * ntiles / nsplit);
+    const int t_hi = (int)((long)(split + 1) * ntiles / nsplit);
+    const int mode = knn_mode(meta, n);
+    const int qrow0 = qb * KNN_TQ;
+    const int myq = qrow0 + 16 * wave + j16;          // block-local query row
+    const long gq = (long)q_base + myq;
+    const double qn = qnorm[myq];
+    const int nfc = n_pad / KNN_BK;
+
+    double L[KL];
+    int I[KL];
+#pragma unroll
+    for (int e = 0; e < KL; e++) { L[e] = KNN_INF; I[e] = -1; }
+    double thr = KNN_INF;
+
+    const int total = (mode == KNN_MODE_SCAN) ? 0 : (t_hi - t_lo) * nfc;
+
+    dbl4 acc[8];
+#pragma unroll
+    for (int mt = 0; mt < 8; mt++) acc[mt] = (dbl4){0.0, 0.0, 0.0, 0.0};
+
+    // wave-uniform LDS bases
+    LDS_AS char *lds = (LDS_AS char *)smem;
+
+    auto stage = [&](int c) {
+        const int t = t_lo + c / nfc, fc = c % nfc, buf = c & 1;
+        const int f = KNN_BK * fc + 2 * g;
+        const double *csrc = cblk + (size_t)(t * KNN_TC + 16 * wave + j16) * n_pad + f;
+        const double *qsrc = qblk + (size_t)(qrow0 + 16 * wave + j16) * n_pad + f;
+        LDS_AS char *cdst = lds + buf * 16384 + wave * 2048;
+        LDS_AS char *qdst = lds + 32768 + buf * 16384 + wave * 2048;
+        __builtin_amdgcn_global_load_lds((const void *)(csrc), (LDS_AS void *)cdst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *)(csrc + 8), (LDS_AS void *)(cdst + 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *)(qsrc), (LDS_AS void *)qdst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *)(qsrc + 8), (LDS_AS void *)(qdst + 1024), 16, 0, 0);
+        if (fc == 0 && wave == 0) {
+            __builtin_amdgcn_global_load_lds((const void *)(cnorm + (size_t)t * KNN_TC + 2 * lane),
+                                             (LDS_AS void *)(lds + 65536 + (t & 1) * 1024), 16, 0, 0);
+        }
+    };
+
+    if (total > 0) {
+        stage(0);
+        __syncthreads();
+    }
+    for (int c = 0; c < total; c++) {
+        const int buf = c & 1;
+        if (c + 1 < total) stage(c + 1);
+        {
+            const LDS_AS dbl2 *cs = (const LDS_AS dbl2 *)(lds + buf * 16384);
+            const LDS_AS dbl2 *qs = (const LDS_AS dbl2 *)(lds + 32768 + buf * 16384 + wave * 2048);
+            dbl2 b0 = qs[lane];
+            dbl2 b1 = qs[64 + lane];
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) {
+                dbl2 a0 = cs[(mt * 2) * 64 + lane];
+                dbl2 a1 = cs[(mt * 2 + 1) * 64 + lane];
+                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, b0.x, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, b0.y, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, b1.x, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, b1.y, acc[mt], 0, 0, 0);
+            }
+        }
+        if ((c % nfc) == nfc - 1) {
+            // ---- epilogue for tile t: d^2, threshold filter, insertion ----
+            const int t = t_lo + c / nfc;
+            const LDS_AS double *cn = (const LDS_AS double *)(lds + 65536 + (t & 1) * 1024);
+            const double lim = L[KL - 1] < thr ? L[KL - 1] : thr;
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) {
+                double d[4];
+                int id[4];
+                unsigned pend = 0;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int lrow = 16 * mt + g + 4 * r;
+                    const int row = t * KNN_TC + lrow;
+                    double v = fma(-2.0, acc[mt][r], qn + cn[lrow]);
+                    const bool valid = (row < nc) && ((long)c_base + row != gq) &&
+                                       !(mode == KNN_MODE_INT && v == 0.0);
+                    d[r] = valid ? v : KNN_INF;
+                    id[r] = (int)(c_base + row);
+                    pend |= (d[r] <= lim) ? (1u << r) : 0u;
+                }
+                while (__ballot(pend != 0) != 0ull) {
+                    const int b = pend ? __builtin_ctz(pend) : 4;
+                    double dd = (b == 0) ? d[0] : (b == 1) ? d[1] : (b == 2) ? d[2] : (b == 3) ? d[3] : KNN_INF;
+                    int ii = (b == 0) ? id[0] : (b == 1) ? id[1] : (b == 2) ? id[2] : id[3];
+                    pend &= pend - 1;
+                    list_insert<KL>(L, I, dd, ii);
+                }
+                acc[mt] = (dbl4){0.0, 0.0, 0.0, 0.0};
+            }
+            // shared threshold of the query's 4 lanes: their union holds
+            // >= KS entries <= max_h L_h[KS/4-1], and every lane already
+            // rejects >= min_h L_h[KL-1]
+            double lmin = L[KL - 1], u = L[KS / 4 - 1];
+            lmin = fmin(lmin, __shfl_xor(lmin, 16));
+            lmin = fmin(lmin, __shfl_xor(lmin, 32));
+            u = fmax(u, __shfl_xor(u, 16));
+            u = fmax(u, __shfl_xor(u, 32));
+            thr = fmin(lmin, u);
+        }
+        __syncthreads();
+    }
+
+    if (myq < nq) {
+        const size_t base = (((size_t)split * nq_pad + myq) * 4 + g) * KL;
+#pragma unroll
+        for (int e = 0; e < KL; e++) {
+            part_d[base + e] = L[e];
+            part_i[base + e] = I[e];
+        }
+        if (g == 0) part_T[(size_t)split * nq_pad + myq] = thr;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_merge: one wave per query.  Lane j < 4*nsplit owns partial list j,
+// lane 4*nsplit the running state; KP+1 rounds of a wave argmin over the
+// heads select the new state (KP entries by (d^2, idx)) and the smallest
+// dropped value, which lowers the rejection bound T.  GEMM mode: entries
+// new in this step get their exact reference-order S from the resident
+// block (the only step at which their rows are on this device).
+// ---------------------------------------------------------------------------
+template <int KL, int KP>
+__global__ __launch_bounds__(256) void k_merge(
+    const double *__restrict__ part_d, const int *__restrict__ part_i,
+    const double *__restrict__ part_T, int nsplit, int nq, int nq_pad, int first_step,
+    double *__restrict__ st_d, double *__restrict__ st_x, int *__restrict__ st_i,
+    double *__restrict__ st_T, const double *__restrict__ qblk,
+    const double *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
+    const double *__restrict__ meta)
+{
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + wave;
+    if (q >= nq) return;
+    const int mode = knn_mode(meta, n);
+    const int nl = 4 * nsplit;
+
+    const double *src_d = nullptr;
+    const int *src_i = nullptr;
+    int len = KP;
+    if (lane < nl) {
+        const int s = lane >> 2, gg = lane & 3;
+        const size_t base = (((size_t)s * nq_pad + q) * 4 + gg) * KL;
+        src_d = part_d + base;
+        src_i = part_i + base;
+        len = KL;
+    } else if (lane == nl && !first_step) {
+        src_d = st_d + (size_t)q * KP;
+        src_i = st_i + (size_t)q * KP;
+    }
+    int pos = 0;
+    double hd = src_d ? src_d[0] : KNN_INF;
+    int hi = src_d ? src_i[0] : 0x7fffffff;
+    if (hd == KNN_INF) hi = 0x7fffffff;
+
+    // T: rejection bound of the lane filters (every candidate a lane turned
+    // away has d^2 >= T); Td: smallest d^2 dropped by a merge (those rank
+    // after every kept entry by (d^2, idx), so only the GEMM certificate
+    // needs them).
+    double T = KNN_INF, Td = KNN_INF;
+    if (lane < nsplit) T = part_T[(size_t)lane * nq_pad + q];
+    if (lane == nl && !first_step) { T = st_T[2 * (size_t)q]; Td = st_T[2 * (size_t)q + 1]; }
+    for (int off = 32; off > 0; off >>= 1) {
+        T = fmin(T, __shfl_xor(T, off));
+        Td = fmin(Td, __shfl_xor(Td, off));
+    }
+
+    double sd = KNN_INF;
+    int si = -1, ssrc = 0, spos = 0;
+    for (int r = 0; r <= KP; r++) {
+        double wd = hd;
+        int wi = hi;
+        wave_argmin(wd, wi);
+        if (wd == KNN_INF) break;  // every remaining head is empty
+        const unsigned long long who = __ballot(hd == wd && hi == wi);
+        const int wl = __builtin_ctzll(who);
+        const int wpos = __shfl(pos, wl);
+        if (r < KP) {
+            if (lane == r) {
+                sd = wd;
+                si = wi;
+                ssrc = (wl == nl && !first_step) ? 1 : 0;
+                spos = wpos;
+            }
+        } else {
+            Td = fmin(Td, wd);
+        }
+        if (lane == wl) {
+            pos++;
+            hd = (pos < len) ? src_d[pos] : KNN_INF;
+            hi = (pos < len) ? src_i[pos] : 0x7fffffff;
+            if (hd == KNN_INF) hi = 0x7fffffff;
+        }
+    }
+
+    double sx = sd;
+    if (lane < KP && mode == KNN_MODE_GEMM && si >= 0) {
+        if (ssrc) {
+            sx = st_x[(size_t)q * KP + spos];
+        } else {
+            const int row = (int)((long)si - (long)c_base);
+            sx = knn_exact_sq(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n);
+        }
+    }
+    // all reads of the old state are done (wave-private query) -> overwrite
+    if (lane < KP) {
+        st_d[(size_t)q * KP + lane] = sd;
+        st_x[(size_t)q * KP + lane] = sx;
+        st_i[(size_t)q * KP + lane] = (sd == KNN_INF) ? -1 : si;
+    }
+    if (lane == 0) { st_T[2 * (size_t)q] = T; st_T[2 * (size_t)q + 1] = Td; }
+    (void)nc;
+}
+
+// ---------------------------------------------------------------------------
+// k_finalize: one wave per query.  Order by (sqrt(S), idx) -- the key the
+// reference keeps (knn-serial.c:86-90) -- drop S == 0, and certify: every
+// candidate outside the state has approx d^2 >= T, hence exact S >= T - E
+// (E bounds the GEMM-form plus the reference's own rounding); if
+// T - E > tau (the k-th kept S, with a margin so sqrt cannot collapse
+// them) nothing unseen can enter the list.  Uncertified queries go to the
+// rescan list.
+// ---------------------------------------------------------------------------
+template <int KP>
+__global__ __launch_bounds__(256) void k_finalize(
+    const double *__restrict__ st_d, const double *__restrict__ st_x,
+    const int *__restrict__ st_i, const double *__restrict__ st_T,
+    const double *__restrict__ qnorm, int nq, int n, int k,
+    const double *__restrict__ meta, knn_neighbour_t *__restrict__ out,
+    int *__restrict__ fail_count, int *__restrict__ fail_list, int *__restrict__ mode_out)
+{
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + wave;
+    const int mode = knn_mode(meta, n);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *mode_out = mode;
+    if (q >= nq) return;
+    knn_neighbour_t *o = out + (size_t)q * k;
+
+    if (mode == KNN_MODE_SCAN) {
+        if (lane == 0) fail_list[atomicAdd(fail_count, 1)] = q;
+        return;
+    }
+    double sd = KNN_INF, sx = KNN_INF;
+    int si = -1;
+    if (lane < KP) {
+        sd = st_d[(size_t)q * KP + lane];
+        sx = st_x[(size_t)q * KP + lane];
+        si = st_i[(size_t)q * KP + lane];
+    }
+    const double T = st_T[2 * (size_t)q], Td = st_T[2 * (size_t)q + 1];
+    if (mode == KNN_MODE_INT) {
+        // state is sorted by exact (d^2, idx) and zeros were never admitted.
+        // A candidate a lane filter turned away has d^2 >= T; with d^2 == T
+        // it may precede the k-th by index, so certify only tau < T.
+        const bool valid = si >= 0 && sd < KNN_INF;
+        const int nnz = __popcll(__ballot(valid));
+        bool ok;
+        if (nnz >= k) ok = (T == KNN_INF) || (__shfl(sd, k - 1) < T);
+        else ok = (T == KNN_INF);
+        if (!ok) {
+            if (lane == 0) fail_list[atomicAdd(fail_count, 1)] = q;
+            return;
+        }
+        if (lane < k) {
+            knn_neighbour_t rec;
+            rec.distance = valid ? sqrt(sd) : KNN_INF;
+            rec.idx = valid ? si + 1 : 0;
+            rec.label = 0;
+            o[lane] = rec;
+        }
+        return;
+    }
+    // GEMM mode
+    const bool valid = (si >= 0) && (sx == sx) && (sx != 0.0) && (sx < KNN_INF);
+    const double key = valid ? sqrt(sx) : KNN_INF;
+    const int kid = valid ? si : 0x7fffffff;
+    int rank = 0;
+    for (int j = 0; j < KP; j++) {
+        double kj = __shfl(key, j);
+        int ij = __shfl(kid, j);
+        rank += (kj < key || (kj == key && ij < kid)) ? 1 : 0;
+    }
+    const int nnz = __popcll(__ballot(valid));
+    const double Tb = fmin(T, Td);
+    bool ok;
+    if (nnz >= k) {
+        const unsigned long long at = __ballot(valid && rank == k - 1);
+        const double tau = __shfl(sx, __builtin_ctzll(at));
+        const double u = 1.1102230246251565e-16;  // 2^-53
+        const double E = 8.0 * (n + 4) * u * (qnorm[q] + meta[KNN_META_MAXNORM]);
+        ok = (Tb == KNN_INF) || ((Tb - E) > tau * (1.0 + 1.7763568394002505e-15));
+    } else {
+        ok = (Tb == KNN_INF);
+    }
+    if (!ok) {
+        if (lane == 0) fail_list[atomicAdd(fail_count, 1)] = q;
+        return;
+    }
+    if (valid && rank < k) {
+        knn_neighbour_t rec;
+        rec.distance = key;
+        rec.idx = si + 1;
+        rec.label = 0;
+        o[rank] = rec;
+    }
+    if (lane >= nnz && lane < k) {
+        knn_neighbour_t rec;
+        rec.distance = KNN_INF;
+        rec.idx = 0;
+        rec.label = 0;
+        o[lane] = rec;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Exact rescan (rare path): one workgroup per unresolved query; thread t
+// scans rows t, t+256, ... with the reference's arithmetic and key
+// (distance = sqrt(S), S != 0), keeps a register list, then the 256 lists
+// and the running rescan list are merged by (distance, idx) in LDS.
+// ---------------------------------------------------------------------------
+template <int KP>
+__global__ __launch_bounds__(256) void k_rescan_step(
+    const int *__restrict__ fail_list, const double *__restrict__ qblk, int n_pad_q,
+    size_t q_base, const double *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
+    double *__restrict__ rs_d, int *__restrict__ rs_i)
+{
+    __shared__ double sh_d[256 + 1][KP];
+    __shared__ int sh_i[256 + 1][KP];
+    __shared__ double red_d[4];
+    __shared__ int red_i[4];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int slot = blockIdx.x;
+    const int q = fail_list[slot];
+    const double *qa = qblk + (size_t)q * n_pad_q;
+    double L[KP];
+    int I[KP];
+#pragma unroll
+    for (int e = 0; e < KP; e++) { L[e] = KNN_INF; I[e] = 0x7fffffff; }
+    for (int row = tid; row < nc; row += 256) {
+        const double S = knn_exact_sq(qa, cblk + (size_t)row * n_pad, n);
+        const double d = sqrt(S);
+        if (d != 0.0) list_insert<KP>(L, I, d, (int)(c_base + row));
+    }
+#pragma unroll
+    for (int e = 0; e < KP; e++) {
+        sh_d[tid][e] = L[e];
+        sh_i[tid][e] = (L[e] == KNN_INF) ? 0x7fffffff : I[e];
+    }
+    if (tid < KP) {
+        double v = rs_d[(size_t)slot * KP + tid];
+        sh_d[256][tid] = v;
+        sh_i[256][tid] = (v == KNN_INF) ? 0x7fffffff : rs_i[(size_t)slot * KP + tid];
+    }
+    __syncthreads();
+    // tournament over 257 sorted lists: thread t owns list t (t == 0 also 256)
+    int pos = 0, pos2 = 0;
+    for (int r = 0; r < KP; r++) {
+        double hd = (pos < KP) ? sh_d[tid][pos] : KNN_INF;
+        int hi = (pos < KP) ? sh_i[tid][pos] : 0x7fffffff;
+        if (tid == 0) {
+            double h2 = (pos2 < KP) ? sh_d[256][pos2] : KNN_INF;
+            int i2 = (pos2 < KP) ? sh_i[256][pos2] : 0x7fffffff;
+            if (h2 < hd || (h2 == hd && i2 < hi)) { hd = h2; hi = i2; }
+        }
+        double wd = hd;
+        int wi = hi;
+        wave_argmin(wd, wi);
+        if (lane == 0) { red_d[wave] = wd; red_i[wave] = wi; }
+        __syncthreads();
+        double bd = red_d[0];
+        int bi = red_i[0];
+        for (int w = 1; w < 4; w++) {
+            if (red_d[w] < bd || (red_d[w] == bd && red_i[w] < bi)) { bd = red_d[w]; bi = red_i[w]; }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            rs_d[(size_t)slot * KP + r] = bd;
+            rs_i[(size_t)slot * KP + r] = (bd == KNN_INF) ? -1 : bi;
+        }
+        if (bd != KNN_INF) {
+            // advance whichever list held the winner (indices are unique)
+            if (pos < KP && sh_i[tid][pos] == bi && sh_d[tid][pos] == bd) pos++;
+            else if (tid == 0 && pos2 < KP && sh_i[256][pos2] == bi && sh_d[256][pos2] == bd) pos2++;
+        }
+    }
+    (void)q_base;
+}
+
+__global__ void k_rescan_init(double *rs_d, int *rs_i, int count)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) { rs_d[i] = KNN_INF; rs_i[i] = -1; }
+}
+
+__global__ void k_rescan_end(const int *__restrict__ fail_list, int nfail, int KP,
+                             const double *__restrict__ rs_d, const int *__restrict__ rs_i,
+                             int k, knn_neighbour_t *__restrict__ out)
+{
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nfail * k) return;
+    const int slot = t / k, r = t % k;
+    const int q = fail_list[slot];
+    knn_neighbour_t rec;
+    const double d = rs_d[(size_t)slot * KP + r];
+    const int id = rs_i[(size_t)slot * KP + r];
+    const bool ok = d < KNN_INF && id >= 0;
+    rec.distance = ok ? d : KNN_INF;
+    rec.idx = ok ? id + 1 : 0;
+    rec.label = 0;
+    out[(size_t)q * k + r] = rec;
+}
+
+// ---------------------------------------------------------------------------
+// C launchers
+// ---------------------------------------------------------------------------
+static int hip_status(void) { return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP; }
+
+extern "C" int knn_launch_pack(double *blk, size_t cap, size_t rows, size_t n,
+                               const double *src, size_t ld, int layout, void *stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    const size_t rp = knn_rows_pad(cap), np = knn_n_pad(n);
+    double *meta = blk + rp * np + rp;
+    if (hipMemsetAsync(meta, 0, KNN_META_DOUBLES * sizeof(double), s) != hipSuccess)
+        return KNN_ERR_HIP;
+    dim3 grid((unsigned)((rp + 63) / 64), (unsigned)((np + 63) / 64));
+    hipLaunchKernelGGL(k_pack, grid, dim3(256), 0, s, blk, rows, rp, (int)n, (int)np, src, ld, layout);
+    unsigned nb = (unsigned)((rp / 4) < 4096 ? (rp / 4) : 4096);
+    if (nb == 0) nb = 1;
+    hipLaunchKernelGGL(k_norms, dim3(nb), dim3(256), 0, s, blk, rows, rp, (int)n, (int)np);
+    return hip_status();
+}
+
+extern "C" int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_t q_base, int nq,
+                                    const double *cblk, size_t c_rows_pad, size_t c_base, int nc,
+                                    int n, const double *meta, int nsplit,
+                                    double *part_d, int *part_i, double *part_T, int nq_pad,
+                                    void *stream)
+{
+    const int np = (int)knn_n_pad(n);
+    const int nqb = (nq + KNN_TQ - 1) / KNN_TQ;
+    const int ntiles = (nc + KNN_TC - 1) / KNN_TC;
+    if (nqb <= 0 || nsplit <= 0) return KNN_ERR_INVALID;
+    // geometry checks the kernel relies on (no out-of-bounds staging)
+    if ((size_t)nqb * KNN_TQ > q_rows_pad || (size_t)ntiles * KNN_TC > c_rows_pad ||
+        nq_pad < nqb * KNN_TQ)
+        return KNN_ERR_INVALID;
+    const double *qnorm = qblk + q_rows_pad * np;
+    const double *cnorm = cblk + c_rows_pad * np;
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP>), dim3((unsigned)(nqb * nsplit)), dim3(512), 0,
+                       (hipStream_t)stream, qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc,
+                       n, np, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad);
+    return hip_status();
+}
+
+extern "C" int knn_launch_merge(const double *part_d, const int *part_i, const double *part_T,
+                                int nsplit, int nq, int nq_pad, int first_step,
+                                double *st_d, double *st_x, int *st_i, double *st_T,
+                                const double *qblk, const double *cblk, size_t c_base, int nc,
+                                int n, const double *meta, void *stream)
+{
+    if (4 * nsplit + 1 > 64) return KNN_ERR_INVALID;
+    const int np = (int)knn_n_pad(n);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<KNN_KL, KNN_KP>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, part_d, part_i, part_T, nsplit, nq, nq_pad,
+                       first_step, st_d, st_x, st_i, st_T, qblk, cblk, c_base, nc, n, np, meta);
+    return hip_status();
+}
+
+extern "C" int knn_launch_finalize(const double *st_d, const double *st_x, const int *st_i,
+                                   const double *st_T, const double *qblk, size_t q_rows_pad,
+                                   int nq, int n, int k, const double *meta,
+                                   knn_neighbour_t *out, int *fail_count, int *fail_list,
+                                   int *mode_out, void *stream)
+{
+    if (k <= 0 || k > KNN_KP) return KNN_ERR_INVALID;
+    const double *qnorm = qblk + q_rows_pad * knn_n_pad(n);
+    hipLaunchKernelGGL(k_finalize<KNN_KP>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, st_d, st_x, st_i, st_T, qnorm, nq, n, k, meta,
+                       out, fail_count, fail_list, mode_out);
+    return hip_status();
+}
+
+extern "C" int knn_launch_rescan_init(double *rs_d, int *rs_i, int nfail, void *stream)
+{
+    const int cnt = nfail * KNN_KP;
+    if (cnt <= 0) return KNN_OK;
+    hipLaunchKernelGGL(k_rescan_init, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, rs_d, rs_i, cnt);
+    return hip_status();
+}
+
+extern "C" int knn_launch_rescan_step(const int *fail_list, int nfail, const double *qblk,
+                                      size_t q_base, const double *cblk, size_t c_base, int nc,
+                                      int n, double *rs_d, int *rs_i, void *stream)
+{
+    if (nfail <= 0) return KNN_OK;
+    const int np = (int)knn_n_pad(n);
+    hipLaunchKernelGGL(k_rescan_step<KNN_KP>, dim3((unsigned)nfail), dim3(256), 0,
+                       (hipStream_t)stream, fail_list, qblk, np, q_base, cblk, c_base, nc, n, np,
+                       rs_d, rs_i);
+    return hip_status();
+}
+
+extern "C" int knn_launch_rescan_end(const int *fail_list, int nfail, const double *rs_d,
+                                     const int *rs_i, int k, knn_neighbour_t *out, void *stream)
+{
+    const int cnt = nfail * k;
+    if (cnt <= 0) return KNN_OK;
+    hipLaunchKernelGGL(k_rescan_end, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, fail_list, nfail, KNN_KP, rs_d, rs_i, k, out);
+    return hip_status();
+}

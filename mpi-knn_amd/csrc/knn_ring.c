@@ -1,0 +1,241 @@
+/*
+ * knn_ring.c -- knn_search() across the GPUs of one node: the corpus-block
+ * ring of mpi-knn-parallel_{blocking,non_blocking}.c rebuilt on RCCL.
+ *
+ * Reference schedule (blk:122-244, nb:132-259): rank r owns rows
+ * [r*R, (r+1)*R), R = m/P (remainder dropped), and passes blocks to r+1
+ * each step with MPI_Send/Recv or Isend/Irecv+Wait, barrier-locked, with no
+ * compute/comm overlap and a broken schedule.
+ *
+ * Here: device g owns queries [g*R, min(m,(g+1)*R)), R = ceil(m/P) (no row
+ * dropped).  Step s computes on block (g - s) mod P while the same block is
+ * sent to g+1 and block (g - s - 1) mod P is received from g-1, on a
+ * separate comm stream per device (ncclSend/ncclRecv over xGMI, one group
+ * per hop) -- double-buffered, so the next block lands while the current
+ * one is being contracted.  Every device visits all P blocks exactly once;
+ * results are byte-identical to the 1-GPU path (merge order is by (d, idx)).
+ * The meta of all blocks is combined with one ncclAllReduce(max).
+ */
+#include "knn_internal.h"
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define KNN_RING_MAX 64
+
+typedef struct {
+    int dev;
+    size_t rows, base;          /* own block */
+    void *qb;                   /* own packed block: the queries, never overwritten */
+    void *bufa, *bufb;          /* receive buffers (capacity R) */
+    void *cur, *nxt, *spare;    /* rotation roles over qb / bufa / bufb */
+    double *src;                /* raw rows of the own block */
+    double *meta;               /* reduced meta (8 doubles) */
+    knn_neighbour_t *d_out;
+    knn_ctx_t *ctx;
+    hipStream_t cs, ms;         /* compute / comm streams */
+    hipEvent_t ev_comp, ev_comm;
+    ncclComm_t comm;
+} ring_dev_t;
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static int ring_hop(ring_dev_t *d, int P, size_t bytes)
+{
+    /* nxt[g] was read by step s-1's compute: the comm waits for it. */
+    for (int g = 0; g < P; g++) {
+        if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
+        if (hipStreamWaitEvent(d[g].ms, d[g].ev_comp, 0) != hipSuccess) return KNN_ERR_HIP;
+    }
+    if (ncclGroupStart() != ncclSuccess) return KNN_ERR_RCCL;
+    for (int g = 0; g < P; g++) {
+        if (ncclSend(d[g].cur, bytes, ncclUint8, (g + 1) % P, d[g].comm, d[g].ms) != ncclSuccess ||
+            ncclRecv(d[g].nxt, bytes, ncclUint8, (g - 1 + P) % P, d[g].comm, d[g].ms) != ncclSuccess) {
+            ncclGroupEnd();
+            return KNN_ERR_RCCL;
+        }
+    }
+    if (ncclGroupEnd() != ncclSuccess) return KNN_ERR_RCCL;
+    for (int g = 0; g < P; g++) {
+        if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
+        if (hipEventRecord(d[g].ev_comm, d[g].ms) != hipSuccess) return KNN_ERR_HIP;
+    }
+    return KNN_OK;
+}
+
+/* One full rotation: at step s device g folds block (g - off - s) mod P,
+ * where off says how far the blocks have already moved. */
+static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int off,
+                     int rescan)
+{
+    int rc;
+    for (int s = 0; s < P; s++) {
+        if (s < P - 1 && (rc = ring_hop(d, P, bytes))) return rc;
+        for (int g = 0; g < P; g++) {
+            const int b = ((g - off - s) % P + P) % P;
+            const size_t base = (size_t)b * R;
+            const size_t rows = (base + R <= m) ? R : m - base;
+            if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
+            rc = rescan ? knn_ctx_rescan_step(d[g].ctx, d[g].cur, rows, base, d[g].cs)
+                        : knn_ctx_step(d[g].ctx, d[g].cur, rows, base, d[g].cs);
+            if (rc) return rc;
+            if (hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) return KNN_ERR_HIP;
+        }
+        if (s < P - 1) {
+            for (int g = 0; g < P; g++) {
+                if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
+                if (hipStreamWaitEvent(d[g].cs, d[g].ev_comm, 0) != hipSuccess) return KNN_ERR_HIP;
+                /* the own block (queries) only ever leaves; it is never a
+                 * receive target, so the two other buffers alternate */
+                void *t = d[g].cur;
+                d[g].cur = d[g].nxt;
+                if (t == d[g].qb) {
+                    d[g].nxt = d[g].spare;
+                } else {
+                    d[g].nxt = t;
+                }
+            }
+        }
+    }
+    return KNN_OK;
+}
+
+int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k, int ngpus,
+                         knn_neighbour_t *out, double *seconds)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KNN_ERR_NODEVICE;
+    if (ngpus > ndev || ngpus > KNN_RING_MAX) return KNN_ERR_NODEVICE;
+    const int P = ngpus;
+    const size_t R = (m + P - 1) / P;
+    if (R == 0 || (size_t)(P - 1) * R >= m) return KNN_ERR_INVALID; /* every block non-empty */
+    const size_t bytes = knn_block_bytes(R, n);
+
+    ring_dev_t d[KNN_RING_MAX];
+    memset(d, 0, sizeof(d));
+    int devs[KNN_RING_MAX];
+    ncclComm_t comms[KNN_RING_MAX];
+    int rc = KNN_OK;
+    for (int g = 0; g < P; g++) devs[g] = g;
+    if (ncclCommInitAll(comms, P, devs) != ncclSuccess) return KNN_ERR_RCCL;
+
+    for (int g = 0; g < P && !rc; g++) {
+        ring_dev_t *e = &d[g];
+        e->dev = g;
+        e->comm = comms[g];
+        e->base = (size_t)g * R;
+        e->rows = (e->base + R <= m) ? R : m - e->base;
+        if (hipSetDevice(g) != hipSuccess) { rc = KNN_ERR_HIP; break; }
+        if (hipStreamCreateWithFlags(&e->cs, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&e->ms, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_comp, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_comm, hipEventDisableTiming) != hipSuccess) {
+            rc = KNN_ERR_HIP;
+            break;
+        }
+        if (hipMalloc(&e->qb, bytes) != hipSuccess || hipMalloc(&e->bufa, bytes) != hipSuccess ||
+            hipMalloc(&e->bufb, bytes) != hipSuccess ||
+            hipMalloc((void **)&e->src, e->rows * n * sizeof(double)) != hipSuccess ||
+            hipMalloc((void **)&e->meta, KNN_META_DOUBLES * sizeof(double)) != hipSuccess ||
+            hipMalloc((void **)&e->d_out, e->rows * (size_t)k * sizeof(knn_neighbour_t)) != hipSuccess) {
+            rc = KNN_ERR_NOMEM;
+            break;
+        }
+        /* own rows to the device: column-major rows are a 2-D sub-matrix */
+        hipError_t he;
+        if (layout == KNN_COLMAJOR)
+            he = hipMemcpy2D(e->src, e->rows * sizeof(double), X + e->base, m * sizeof(double),
+                             e->rows * sizeof(double), n, hipMemcpyHostToDevice);
+        else
+            he = hipMemcpy(e->src, X + e->base * n, e->rows * n * sizeof(double),
+                           hipMemcpyHostToDevice);
+        if (he != hipSuccess) { rc = KNN_ERR_HIP; break; }
+        rc = knn_ctx_create(&e->ctx, g, e->rows, n, R, k);
+    }
+    for (int g = 0; g < P && !rc; g++)
+        if (hipSetDevice(g) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = KNN_ERR_HIP;
+
+    const double t0 = now_s();
+    /* pack own block (blk:100-109) and reduce the meta over the ring */
+    for (int g = 0; g < P && !rc; g++) {
+        ring_dev_t *e = &d[g];
+        hipSetDevice(g);
+        e->cur = e->qb;
+        e->nxt = e->bufa;
+        e->spare = e->bufb;
+        rc = knn_block_pack(e->qb, R, e->rows, n, e->src, layout == KNN_COLMAJOR ? e->rows : n,
+                            layout, e->cs);
+        if (!rc && hipMemcpyAsync(e->meta, (char *)e->qb + knn_block_meta_offset(R, n),
+                                  KNN_META_DOUBLES * sizeof(double), hipMemcpyDeviceToDevice,
+                                  e->cs) != hipSuccess)
+            rc = KNN_ERR_HIP;
+    }
+    if (!rc) {
+        if (ncclGroupStart() != ncclSuccess) rc = KNN_ERR_RCCL;
+        for (int g = 0; g < P && !rc; g++)
+            if (ncclAllReduce(d[g].meta, d[g].meta, KNN_META_DOUBLES, ncclFloat64, ncclMax,
+                              d[g].comm, d[g].cs) != ncclSuccess)
+                rc = KNN_ERR_RCCL;
+        if (ncclGroupEnd() != ncclSuccess && !rc) rc = KNN_ERR_RCCL;
+    }
+    for (int g = 0; g < P && !rc; g++) {
+        hipSetDevice(g);
+        rc = knn_ctx_begin(d[g].ctx, d[g].qb, R, d[g].base, d[g].meta, d[g].cs);
+        if (!rc && hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
+    }
+    if (!rc) rc = ring_pass(d, P, R, m, bytes, 0, 0);
+    size_t unresolved_total = 0;
+    for (int g = 0; g < P && !rc; g++) {
+        size_t u = 0;
+        hipSetDevice(g);
+        rc = knn_ctx_end(d[g].ctx, d[g].d_out, &u, d[g].cs);
+        unresolved_total += u;
+    }
+    if (!rc && unresolved_total) {
+        /* A pass makes P-1 hops, so device g now holds block g+1; rotate
+         * once more for the exact rescan of uncertified queries. */
+        for (int g = 0; g < P && !rc; g++) {
+            hipSetDevice(g);
+            if (hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
+        }
+        if (!rc) rc = ring_pass(d, P, R, m, bytes, P - 1, 1);
+        for (int g = 0; g < P && !rc; g++) {
+            hipSetDevice(g);
+            rc = knn_ctx_rescan_end(d[g].ctx, d[g].d_out, d[g].cs);
+        }
+    }
+    for (int g = 0; g < P && !rc; g++)
+        if (hipSetDevice(g) != hipSuccess || hipStreamSynchronize(d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
+    if (seconds) *seconds = now_s() - t0;
+    for (int g = 0; g < P && !rc; g++) {
+        hipSetDevice(g);
+        if (hipMemcpy(out + d[g].base * (size_t)k, d[g].d_out,
+                      d[g].rows * (size_t)k * sizeof(knn_neighbour_t), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = KNN_ERR_HIP;
+    }
+
+    for (int g = 0; g < P; g++) {
+        hipSetDevice(g);
+        if (d[g].ctx) knn_ctx_destroy(d[g].ctx);
+        hipFree(d[g].qb);
+        hipFree(d[g].bufa);
+        hipFree(d[g].bufb);
+        hipFree(d[g].src);
+        hipFree(d[g].meta);
+        hipFree(d[g].d_out);
+        if (d[g].ev_comp) hipEventDestroy(d[g].ev_comp);
+        if (d[g].ev_comm) hipEventDestroy(d[g].ev_comm);
+        if (d[g].cs) hipStreamDestroy(d[g].cs);
+        if (d[g].ms) hipStreamDestroy(d[g].ms);
+        ncclCommDestroy(comms[g]);
+    }
+    return rc;
+}

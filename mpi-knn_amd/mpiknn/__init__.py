@@ -1,0 +1,259 @@
+"""mpiknn -- Python host mirror of libknn (include/knn.h) over ctypes.
+
+The product is the C-ABI library ``mpi-knn_amd/lib/libknn.so`` (HIP kernels
+for gfx950 + a C host engine).  This module only binds it: numpy arrays for
+the host API, raw device pointers (e.g. ``torch.Tensor.data_ptr()``) for the
+device-resident API used by the per-rank RCCL ring (``mpiknn.ring``) and by
+bench.py.  There is no CPU fallback: if the library is missing, importing
+this module raises.
+
+Reference (yiapou13/mpi-knn): serial:L = knn-serial.c,
+blk:L = mpi-knn-parallel_blocking.c, nb:L = mpi-knn-parallel_non_blocking.c.
+"""
+import atexit
+import ctypes
+import os
+import sys
+import weakref
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libknn.so")
+
+# knn_neighbour_t (blk:15-20): {double distance; int32 idx (1-based); int32 label}
+NB_DTYPE = np.dtype([("distance", "<f8"), ("idx", "<i4"), ("label", "<i4")])
+
+OK, ERR_INVALID, ERR_NOMEM, ERR_HIP, ERR_IO, ERR_FORMAT, ERR_UNSUPPORTED, ERR_NODEVICE, ERR_RCCL = range(9)
+COLMAJOR, ROWMAJOR = 0, 1
+F64, F32 = 0, 1
+VOTE_SERIAL, VOTE_MPI, VOTE_MAJORITY = 0, 1, 2
+MAX_K = 32
+META_DOUBLES = 8
+MODE_NAMES = {0: "int-exact", 1: "gemm+rerank", 2: "exact-scan"}
+
+# every symbol include/knn.h declares (checked by tests/test_abi.py)
+API_SYMBOLS = (
+    "knn_strerror", "knn_load_mat", "knn_free", "knn_search", "knn_last_search_seconds",
+    "knn_classify", "knn_block_bytes", "knn_block_meta_offset", "knn_block_pack",
+    "knn_ctx_create", "knn_ctx_destroy", "knn_ctx_begin", "knn_ctx_step", "knn_ctx_end",
+    "knn_ctx_rescan_step", "knn_ctx_rescan_end", "knn_search_packed", "knn_ctx_info",
+    "knn_ctx_profile",
+)
+
+
+class KnnError(RuntimeError):
+    def __init__(self, status, what=""):
+        self.status = status
+        super().__init__("%s: %s (status %d)" % (what, strerror(status), status))
+
+
+def _share_torch_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own
+    libamdhip64/librccl with the same sonames as /opt/rocm's; if libknn
+    pulled in the system copies first, torch would later load a second HIP
+    runtime and find no GPU.  Pre-load torch's copies (by path, without
+    importing torch) so libknn binds to them; without torch the system
+    ROCm libraries are used."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    tlib = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    for name in ("libamdhip64.so", "librccl.so"):
+        path = os.path.join(tlib, name)
+        if os.path.exists(path):
+            ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libknn not built: %s missing (run `make -C mpi-knn_amd` or "
+                          "__graft_entry__.build())" % LIB_PATH)
+    _share_torch_runtime()
+    L = ctypes.CDLL(LIB_PATH)
+    p, sz, i, d = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    psz = ctypes.POINTER(ctypes.c_size_t)
+    sig = {
+        "knn_strerror": ([i], ctypes.c_char_p),
+        "knn_load_mat": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, pp, psz, psz, pp, psz], i),
+        "knn_free": ([p], None),
+        "knn_search": ([p, sz, sz, i, p, i, i, i, p], i),
+        "knn_last_search_seconds": ([], d),
+        "knn_classify": ([p, sz, i, i, i, p, p, psz], i),
+        "knn_block_bytes": ([sz, sz], sz),
+        "knn_block_meta_offset": ([sz, sz], sz),
+        "knn_block_pack": ([p, sz, sz, sz, p, sz, i, p], i),
+        "knn_ctx_create": ([pp, i, sz, sz, sz, i], i),
+        "knn_ctx_destroy": ([p], i),
+        "knn_ctx_begin": ([p, p, sz, sz, p, p], i),
+        "knn_ctx_step": ([p, p, sz, sz, p], i),
+        "knn_ctx_end": ([p, p, psz, p], i),
+        "knn_ctx_rescan_step": ([p, p, sz, sz, p], i),
+        "knn_ctx_rescan_end": ([p, p, p], i),
+        "knn_search_packed": ([p, p, sz, p, p], i),
+        "knn_ctx_info": ([p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], i),
+        "knn_ctx_profile": ([p, i, ctypes.POINTER(d), ctypes.POINTER(d), ctypes.POINTER(i)], i),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    return L
+
+
+lib = _load()
+
+
+def strerror(status):
+    return lib.knn_strerror(status).decode()
+
+
+def _check(rc, what):
+    if rc != OK:
+        raise KnnError(rc, what)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ---------------------------------------------------------------- host API
+
+def load_mat(path, xvar="train_X", lvar="train_labels"):
+    """knn_load_mat (replaces matOpen/matGetVariable/mxGetPr, serial:40-52).
+
+    Returns (X (m, n) float64 -- a C-ordered copy of the column-major data,
+    labels (numel,) float64 or None)."""
+    Xp, Lp = ctypes.c_void_p(), ctypes.c_void_p()
+    m, n, nl = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    rc = lib.knn_load_mat(path.encode(), xvar.encode(), lvar.encode() if lvar else None,
+                          ctypes.byref(Xp), ctypes.byref(m), ctypes.byref(n),
+                          ctypes.byref(Lp), ctypes.byref(nl))
+    _check(rc, "knn_load_mat(%s)" % path)
+    try:
+        cnt = m.value * n.value
+        flat = np.ctypeslib.as_array(ctypes.cast(Xp, ctypes.POINTER(ctypes.c_double)),
+                                     shape=(max(cnt, 1),))[:cnt].copy()
+        X = flat.reshape((n.value, m.value)).T.copy()  # column-major m x n
+        labels = None
+        if Lp.value:
+            labels = np.ctypeslib.as_array(ctypes.cast(Lp, ctypes.POINTER(ctypes.c_double)),
+                                           shape=(max(nl.value, 1),))[:nl.value].copy()
+    finally:
+        lib.knn_free(Xp)
+        lib.knn_free(Lp)
+    return X, labels
+
+
+def search(X, k=30, ngpus=1, labels=None, layout="row"):
+    """knn_search: all-kNN with the reference's serial semantics.
+
+    X: (m, n) float64.  layout="row" passes C order, "col" Fortran order (the
+    .mat layout).  Returns (neighbours (m, k) NB_DTYPE, search seconds)."""
+    X = np.asarray(X, dtype=np.float64)
+    m, n = X.shape
+    if layout == "col":
+        buf, lay = np.asfortranarray(X), COLMAJOR
+    else:
+        buf, lay = np.ascontiguousarray(X), ROWMAJOR
+    out = np.zeros((m, k), dtype=NB_DTYPE)
+    lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.float64)
+    rc = lib.knn_search(_ptr(buf), m, n, lay, _ptr(lab), k, ngpus, F64, _ptr(out))
+    _check(rc, "knn_search")
+    return out, lib.knn_last_search_seconds()
+
+
+def classify(nb, labels, nclasses=10, rule=VOTE_SERIAL):
+    """knn_classify (serial:104-130 / blk:252-270).  Returns (pred, matches)."""
+    nb = np.ascontiguousarray(nb)
+    m, k = nb.shape
+    lab = np.ascontiguousarray(labels, dtype=np.float64)
+    pred = np.zeros(m, dtype=np.int32)
+    matches = ctypes.c_size_t()
+    rc = lib.knn_classify(_ptr(nb), m, k, nclasses, rule, _ptr(lab), _ptr(pred), ctypes.byref(matches))
+    _check(rc, "knn_classify")
+    return pred, matches.value
+
+
+# ------------------------------------------------------ device-resident API
+
+def block_bytes(cap, n):
+    return lib.knn_block_bytes(cap, n)
+
+
+def block_meta_offset(cap, n):
+    return lib.knn_block_meta_offset(cap, n)
+
+
+def block_pack(d_block, cap, rows, n, d_src, ld, layout, stream=0):
+    """knn_block_pack on device pointers (ints).  layout COLMAJOR/ROWMAJOR."""
+    _check(lib.knn_block_pack(d_block, cap, rows, n, d_src, ld, layout, stream or None),
+           "knn_block_pack")
+
+
+_live_contexts = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all():
+    # release device buffers while the HIP runtime is still up (its own
+    # teardown runs after Python's atexit handlers)
+    for c in list(_live_contexts):
+        c.close()
+
+
+class Context:
+    """knn_ctx_t: running neighbour lists of nq queries on one device."""
+
+    def __init__(self, device, nq, n, block_cap, k):
+        self._h = ctypes.c_void_p()
+        _check(lib.knn_ctx_create(ctypes.byref(self._h), device, nq, n, block_cap, k),
+               "knn_ctx_create")
+        self.nq, self.n, self.block_cap, self.k = nq, n, block_cap, k
+        _live_contexts.add(self)
+
+    def close(self):
+        if self._h:
+            lib.knn_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        if not sys.is_finalizing():
+            self.close()
+
+    def begin(self, d_qblock, q_cap, q_base, d_meta, stream=0):
+        _check(lib.knn_ctx_begin(self._h, d_qblock, q_cap, q_base, d_meta, stream or None),
+               "knn_ctx_begin")
+
+    def step(self, d_cblock, nc, c_base, stream=0):
+        _check(lib.knn_ctx_step(self._h, d_cblock, nc, c_base, stream or None), "knn_ctx_step")
+
+    def end(self, d_out, stream=0):
+        u = ctypes.c_size_t()
+        _check(lib.knn_ctx_end(self._h, d_out, ctypes.byref(u), stream or None), "knn_ctx_end")
+        return u.value
+
+    def rescan_step(self, d_cblock, nc, c_base, stream=0):
+        _check(lib.knn_ctx_rescan_step(self._h, d_cblock, nc, c_base, stream or None),
+               "knn_ctx_rescan_step")
+
+    def rescan_end(self, d_out, stream=0):
+        _check(lib.knn_ctx_rescan_end(self._h, d_out, stream or None), "knn_ctx_rescan_end")
+
+    def search_packed(self, d_block, m, d_out, stream=0):
+        _check(lib.knn_search_packed(self._h, d_block, m, d_out, stream or None),
+               "knn_search_packed")
+
+    def profile(self, enable=-1):
+        """knn_ctx_profile: (dist_ms, merge_ms, launches); enable 1 resets+starts."""
+        dm, mm, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        _check(lib.knn_ctx_profile(self._h, enable, ctypes.byref(dm), ctypes.byref(mm),
+                                   ctypes.byref(n)), "knn_ctx_profile")
+        return dm.value, mm.value, n.value
+
+    def info(self):
+        mode, splits = ctypes.c_int(), ctypes.c_int()
+        _check(lib.knn_ctx_info(self._h, ctypes.byref(mode), ctypes.byref(splits)), "knn_ctx_info")
+        return mode.value, splits.value

@@ -1,0 +1,132 @@
+"""Per-rank corpus-block ring over torch.distributed (RCCL on ROCm).
+
+The multi-process counterpart of knn_ring.c, used when one process drives
+one GPU (bench.py under torch.distributed.run).  It replaces the MPI ring of
+mpi-knn-parallel_blocking.c:122-244 / _non_blocking.c:132-259:
+
+* rank g owns query rows [g*R, min(m, (g+1)*R)), R = ceil(m/P) (the
+  reference uses floor(m/P) and drops the remainder, blk:81);
+* step s folds block (g - s) mod P; the hop for step s+1 (isend to g+1,
+  irecv from g-1) is posted BEFORE step s's kernels, so the transfer runs
+  on RCCL's stream while the current block is contracted (the reference
+  waits for every hop before computing);
+* the own packed block stays resident as the query block; two receive
+  buffers alternate (every rank visits all P blocks exactly once -- the
+  reference visits r, r-2, ..., r-P and never r-1);
+* the block meta is combined with one all_reduce(MAX) of 8 doubles.
+
+The engine object does the per-block work (GpuEngine: libknn kernels on the
+current HIP stream).  Tests substitute a CPU engine to check the schedule
+under gloo.
+"""
+import numpy as np
+
+
+def partition(m, P):
+    """Block b = rows [b*R, min(m, (b+1)*R)), R = ceil(m/P)."""
+    R = -(-m // P)
+    blocks = []
+    for b in range(P):
+        lo = min(b * R, m)
+        hi = min((b + 1) * R, m)
+        blocks.append((lo, hi - lo))
+    return R, blocks
+
+
+class GpuEngine:
+    """libknn on one device; buffers are torch uint8 tensors on cuda."""
+
+    def __init__(self, torch, device, n, R, nq, k):
+        import mpiknn
+        self.torch, self.mk = torch, mpiknn
+        self.dev = torch.device("cuda", device)
+        self.n, self.R, self.nq, self.k = n, R, nq, k
+        nb = mpiknn.block_bytes(R, n)
+        self.qb = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
+        self.bufa = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+        self.bufb = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+        self.meta_off = mpiknn.block_meta_offset(R, n)
+        self.meta = torch.zeros(mpiknn.META_DOUBLES, dtype=torch.float64, device=self.dev)
+        self.out = torch.zeros(max(nq, 1) * k * 16, dtype=torch.uint8, device=self.dev)
+        self.ctx = mpiknn.Context(device, max(nq, 1), n, R, k)
+
+    def stream(self):
+        return self.torch.cuda.current_stream(self.dev).cuda_stream
+
+    def pack(self, src, layout_col):
+        """src: this rank's rows on the device, (rows, n) float64 (any strides
+        matching the layout: col-major -> src.t() contiguous)."""
+        rows = src.shape[0]
+        if layout_col:
+            assert src.stride(0) == 1
+            ld = src.stride(1)
+            lay = self.mk.COLMAJOR
+        else:
+            assert src.stride(1) == 1
+            ld = src.stride(0)
+            lay = self.mk.ROWMAJOR
+        self.mk.block_pack(self.qb.data_ptr(), self.R, rows, self.n, src.data_ptr(), ld, lay,
+                           self.stream())
+        self.meta.copy_(self.qb[self.meta_off:self.meta_off + 8 * self.mk.META_DOUBLES]
+                        .view(self.torch.float64))
+
+    def begin(self, q_base):
+        self.ctx.begin(self.qb.data_ptr(), self.R, q_base, self.meta.data_ptr(), self.stream())
+
+    def step(self, buf, rows, base, rescan=False):
+        if rescan:
+            self.ctx.rescan_step(buf.data_ptr(), rows, base, self.stream())
+        else:
+            self.ctx.step(buf.data_ptr(), rows, base, self.stream())
+
+    def end(self):
+        return self.ctx.end(self.out.data_ptr(), self.stream())
+
+    def rescan_end(self):
+        self.ctx.rescan_end(self.out.data_ptr(), self.stream())
+
+    def result(self):
+        host = self.out.cpu().numpy()
+        return host.view(self.mk.NB_DTYPE).reshape(-1, self.k)[: self.nq]
+
+
+def ring_search(dist, torch, engine, rank, P, m, q_base):
+    """Run the ring on this rank.  `engine` holds the packed own block
+    (engine.pack done).  Collective calls: all_reduce(meta), P-1 hops per
+    pass, all_reduce(unresolved).  Returns the number of queries that took
+    the exact rescan pass on this rank."""
+    R, blocks = partition(m, P)
+    if P > 1:
+        dist.all_reduce(engine.meta, op=dist.ReduceOp.MAX)
+    engine.begin(q_base)
+
+    state = {"cur": engine.qb, "nxt": engine.bufa, "spare": engine.bufb}
+
+    def one_pass(off, rescan):
+        for s in range(P):
+            reqs = []
+            if s < P - 1:
+                ops = [dist.P2POp(dist.isend, state["cur"], (rank + 1) % P),
+                       dist.P2POp(dist.irecv, state["nxt"], (rank - 1) % P)]
+                reqs = dist.batch_isend_irecv(ops)
+            b = (rank - off - s) % P
+            base, rows = blocks[b]
+            engine.step(state["cur"], rows, base, rescan)
+            for r in reqs:
+                r.wait()
+            if s < P - 1:
+                old = state["cur"]
+                state["cur"] = state["nxt"]
+                state["nxt"] = state["spare"] if old is engine.qb else old
+
+    one_pass(0, False)
+    unresolved = engine.end()
+    total = unresolved
+    if P > 1:
+        t = torch.tensor([float(unresolved)], dtype=torch.float64, device=engine.meta.device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        total = int(t.item())
+    if total > 0:
+        one_pass(P - 1, True)
+        engine.rescan_end()
+    return unresolved

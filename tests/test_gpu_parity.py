@@ -1,0 +1,150 @@
+"""GPU parity: libknn (HIP, gfx950) vs the CPU oracle on the same inputs.
+
+The bar: neighbour indices bit-exact and distances
+bit-exact (the reference's own fp64 sqrt(S), S accumulated in j order
+without FMA) for every engine mode -- integer data (exact GEMM form),
+real-valued data (GEMM filter + exact re-rank), non-finite data (exact
+scan) -- and for every block count of the ring.
+"""
+import numpy as np
+import pytest
+
+import datasets
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_same(got, ref, what=""):
+    assert got.shape == ref.shape, what
+    bad_i = np.nonzero(got["idx"] != ref["idx"])
+    assert bad_i[0].size == 0, "%s: %d idx mismatches, first at %s: got %s ref %s" % (
+        what, bad_i[0].size, (bad_i[0][0], bad_i[1][0]), got[bad_i[0][0]][:8], ref[bad_i[0][0]][:8])
+    gd = got["distance"].view(np.uint64)
+    rd = ref["distance"].view(np.uint64)
+    nd = int((gd != rd).sum())
+    assert nd == 0, "%s: %d distance bit mismatches" % (what, nd)
+
+
+def test_digits_integer_mode(knn, oracle):
+    X, y = datasets.digits()
+    ref = oracle.knn(X, 30, labels=y)
+    got, _ = knn.search(X, 30, labels=y)
+    assert_same(got, ref, "digits")
+    # pinned to the reference's own run
+    assert knn.classify(got, y, 10, knn.VOTE_SERIAL)[1] == 1636
+    assert knn.classify(got, y, 10, knn.VOTE_MPI)[1] == 1635
+    assert knn.classify(got, y, 10, knn.VOTE_MAJORITY)[1] == 1742
+
+
+def test_digits_colmajor_layout(knn, oracle):
+    X, y = datasets.digits()
+    ref = oracle.knn(X, 30)
+    got, _ = knn.search(X, 30, layout="col")
+    assert_same(got, ref, "digits col-major")
+
+
+def test_digits_real_gemm_mode(knn, oracle):
+    X, y = datasets.digits_real()
+    ref = oracle.knn(X, 30, labels=y)
+    got, _ = knn.search(X, 30, labels=y)
+    assert_same(got, ref, "digits_real")
+    assert knn.classify(got, y, 10, knn.VOTE_SERIAL)[1] == 1631
+
+
+@pytest.mark.parametrize("m,n,k", [(3000, 784, 30), (1000, 100, 30), (700, 17, 5), (300, 1, 30)])
+def test_mnist_like_integer(knn, oracle, m, n, k):
+    X, y = datasets.mnist_like(m, n, seed=m + n)
+    ref = oracle.knn(X, k)
+    got, _ = knn.search(X, k)
+    assert_same(got, ref, "mnist_like %dx%d k=%d" % (m, n, k))
+
+
+@pytest.mark.parametrize("m,n", [(2000, 64), (513, 200), (129, 3)])
+def test_gaussian_real(knn, oracle, m, n):
+    rng = np.random.default_rng(m * 7 + n)
+    X = rng.normal(0, 1, (m, n))
+    ref = oracle.knn(X, 30)
+    got, _ = knn.search(X, 30)
+    assert_same(got, ref, "gaussian %dx%d" % (m, n))
+
+
+def test_fewer_rows_than_k(knn, oracle):
+    X = np.arange(40, dtype=np.float64).reshape(10, 4)
+    ref = oracle.knn(X, 30)
+    got, _ = knn.search(X, 30)
+    assert_same(got, ref, "m<k")
+    assert (got["idx"][:, 9:] == 0).all() and np.isinf(got["distance"][:, 9:]).all()
+
+
+def test_single_row(knn, oracle):
+    X = np.ones((1, 5))
+    got, _ = knn.search(X, 3)
+    assert (got["idx"] == 0).all() and np.isinf(got["distance"]).all()
+
+
+def test_duplicates_excluded(knn, oracle):
+    X, _ = datasets.digits()
+    X = np.vstack([X, X[:50], X[:50]])  # two extra copies of 50 rows
+    ref = oracle.knn(X, 30)
+    got, _ = knn.search(X, 30)
+    assert_same(got, ref, "duplicates (int)")
+    Xr = X / 7.0 + 0.001
+    ref = oracle.knn(Xr, 30)
+    got, _ = knn.search(Xr, 30)
+    assert_same(got, ref, "duplicates (real)")
+
+
+def test_heavy_ties(knn, oracle):
+    # tiny integer alphabet: huge numbers of exact distance ties
+    rng = np.random.default_rng(5)
+    X = rng.integers(0, 2, (1500, 12)).astype(np.float64)
+    ref = oracle.knn(X, 30)
+    got, _ = knn.search(X, 30)
+    assert_same(got, ref, "binary ties")
+
+
+def test_nonfinite_scan_mode(knn, oracle):
+    rng = np.random.default_rng(3)
+    X = rng.normal(0, 1, (400, 20))
+    X[5, 3] = np.nan
+    X[17, 0] = np.inf
+    ref = oracle.knn(X, 30)
+    got, _ = knn.search(X, 30)
+    assert_same(got, ref, "nan/inf")
+
+
+def test_ring_blocks_match_single_device(knn, oracle):
+    """The ring's per-rank work simulated on one GPU: every block count
+    gives byte-identical results to the 1-block search."""
+    import torch
+    import mpiknn.ring as ring
+
+    for X in (datasets.mnist_like(2500, 784, seed=9)[0], datasets.digits_real()[0]):
+        m, n = X.shape
+        full, _ = knn.search(X, 30)
+        dev = torch.device("cuda", 0)
+        Xd = torch.from_numpy(X).to(dev)
+        for P in (2, 3, 8):
+            R, blocks = ring.partition(m, P)
+            engines = []
+            for g in range(P):
+                base, rows = blocks[g]
+                e = ring.GpuEngine(torch, 0, n, R, rows, 30)
+                e.pack(Xd[base:base + rows], layout_col=False)
+                engines.append(e)
+            meta = torch.stack([e.meta for e in engines]).max(dim=0).values
+            for g, e in enumerate(engines):
+                e.meta.copy_(meta)
+                base, rows = blocks[g]
+                e.begin(base)
+                for s in range(P):
+                    b = (g - s) % P
+                    e.step(engines[b].qb, blocks[b][1], blocks[b][0])
+                u = e.end()
+                if u:
+                    for s in range(P):
+                        b = (g - s) % P
+                        e.step(engines[b].qb, blocks[b][1], blocks[b][0], rescan=True)
+                    e.rescan_end()
+                got = e.result()
+                assert_same(got, full[base:base + rows], "ring P=%d rank %d" % (P, g))
