@@ -30,6 +30,12 @@
 extern "C" {
 #endif
 
+/* Only the entry points below are exported (libknn builds with
+ * -fvisibility=hidden). */
+#ifndef KNN_API
+#define KNN_API __attribute__((visibility("default")))
+#endif
+
 /* blk:15-20 {double distance; int idx; int label;}.  serial:14-18 has the
  * same size and offsets for {distance, idx}. */
 typedef struct {
@@ -57,7 +63,7 @@ enum knn_vote   { KNN_VOTE_SERIAL = 0, KNN_VOTE_MPI = 1, KNN_VOTE_MAJORITY = 2 }
 /* Largest k served (the reference fixes NN = 30, serial:8 / blk:9). */
 #define KNN_MAX_K 32
 
-const char *knn_strerror(int status);
+KNN_API const char *knn_strerror(int status);
 
 /* ---------------------------------------------------------------------- *
  * Ingest -- replaces matOpen / matGetVariable / mxGetM / mxGetN / mxGetPr /
@@ -67,9 +73,9 @@ const char *knn_strerror(int status);
  * *X is column-major m x n (like mxGetPr of train_X), *labels has the
  * numel of lvar (m x 1).  lvar may be NULL.  Free both with knn_free().
  * ---------------------------------------------------------------------- */
-int  knn_load_mat(const char *path, const char *xvar, const char *lvar,
+KNN_API int  knn_load_mat(const char *path, const char *xvar, const char *lvar,
                   double **X, size_t *m, size_t *n, double **labels, size_t *nlabels);
-void knn_free(void *p);
+KNN_API void knn_free(void *p);
 
 /* ---------------------------------------------------------------------- *
  * One-call search on host arrays -- replaces the search section of
@@ -79,14 +85,14 @@ void knn_free(void *p);
  * ngpus > 1; results are byte-identical for every ngpus); dtype must be
  * KNN_F64 in this build.  out: caller-owned m*k records.
  * ---------------------------------------------------------------------- */
-int knn_search(const double *X, size_t m, size_t n, int layout,
+KNN_API int knn_search(const double *X, size_t m, size_t n, int layout,
                const double *labels, int k, int ngpus, int dtype,
                knn_neighbour_t *out);
 
 /* Search wall time of the last knn_search() on this thread, seconds: the
  * span the reference times (serial:70-98, blk:120-250) -- device compute
  * only, excluding load, H2D, D2H and vote. */
-double knn_last_search_seconds(void);
+KNN_API double knn_last_search_seconds(void);
 
 /* ---------------------------------------------------------------------- *
  * Vote + accuracy -- replaces serial:104-130 (rule SERIAL), blk:252-270 /
@@ -96,7 +102,7 @@ double knn_last_search_seconds(void);
  * prediction equals their own label.  Empty slots (idx 0) are skipped where
  * the reference would read out of bounds.
  * ---------------------------------------------------------------------- */
-int knn_classify(const knn_neighbour_t *nb, size_t m, int k, int nclasses,
+KNN_API int knn_classify(const knn_neighbour_t *nb, size_t m, int k, int nclasses,
                  int vote_rule, const double *labels, int *pred, size_t *matches);
 
 /* ---------------------------------------------------------------------- *
@@ -114,64 +120,64 @@ int knn_classify(const knn_neighbour_t *nb, size_t m, int k, int nclasses,
  * ---------------------------------------------------------------------- */
 #define KNN_META_DOUBLES 8
 
-size_t knn_block_bytes(size_t cap, size_t n);
+KNN_API size_t knn_block_bytes(size_t cap, size_t n);
 /* Offset (bytes) of the meta doubles inside a packed block.  The meta of
  * all blocks of one search must be MAX-reduced into the d_meta passed to
  * knn_ctx_begin (a one-shot all-reduce of 8 doubles across ranks). */
-size_t knn_block_meta_offset(size_t cap, size_t n);
+KNN_API size_t knn_block_meta_offset(size_t cap, size_t n);
 
 /* Pack rows (<= cap) points from a device source.  layout KNN_COLMAJOR:
  * element (i, j) at d_src[i + j*ld] (ld >= rows; the .mat layout,
  * serial:82); KNN_ROWMAJOR: d_src[i*ld + j] (ld >= n; blk:81-109).
  * Computes norms and meta.  Replaces blk:100-109 / nb:110-119. */
-int knn_block_pack(void *d_block, size_t cap, size_t rows, size_t n, const double *d_src,
+KNN_API int knn_block_pack(void *d_block, size_t cap, size_t rows, size_t n, const double *d_src,
                    size_t ld, int layout, void *stream);
 
 typedef struct knn_ctx knn_ctx_t;
 
 /* nq queries of dimension n; corpus blocks are packed with capacity
  * block_cap (knn_block_pack's cap) and hold at most block_cap rows. */
-int knn_ctx_create(knn_ctx_t **ctx, int device, size_t nq, size_t n,
+KNN_API int knn_ctx_create(knn_ctx_t **ctx, int device, size_t nq, size_t n,
                    size_t block_cap, int k);
-int knn_ctx_destroy(knn_ctx_t *ctx);
+KNN_API int knn_ctx_destroy(knn_ctx_t *ctx);
 
 /* Start: the queries are the first nq rows of packed block d_qblock
  * (capacity q_cap) with global ids q_base..q_base+nq-1; d_meta = the
  * max-reduced meta of every corpus block. */
-int knn_ctx_begin(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap, size_t q_base,
+KNN_API int knn_ctx_begin(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap, size_t q_base,
                   const double *d_meta, void *stream);
 
 /* Fold one packed corpus block (nc rows, global ids c_base..) into the
  * running neighbour lists.  Blocks may come in any order (ring order). */
-int knn_ctx_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
+KNN_API int knn_ctx_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
                  size_t c_base, void *stream);
 
 /* Finish: write nq*k records to d_out.  Returns in *unresolved (host; the
  * call synchronises the stream) the number of queries whose candidate set
  * could not be certified exact; if > 0 the caller runs one more pass over
  * every block with knn_ctx_rescan_step() then knn_ctx_rescan_end(). */
-int knn_ctx_end(knn_ctx_t *ctx, knn_neighbour_t *d_out, size_t *unresolved,
+KNN_API int knn_ctx_end(knn_ctx_t *ctx, knn_neighbour_t *d_out, size_t *unresolved,
                 void *stream);
-int knn_ctx_rescan_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
+KNN_API int knn_ctx_rescan_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
                         size_t c_base, void *stream);
-int knn_ctx_rescan_end(knn_ctx_t *ctx, knn_neighbour_t *d_out, void *stream);
+KNN_API int knn_ctx_rescan_end(knn_ctx_t *ctx, knn_neighbour_t *d_out, void *stream);
 
 /* Convenience: the whole single-device pipeline on one packed block of
  * capacity m (queries == corpus == rows 0..m-1), including the rescan pass
  * when needed.  ctx must have nq == block_cap == m. */
-int knn_search_packed(knn_ctx_t *ctx, const void *d_block, size_t m,
+KNN_API int knn_search_packed(knn_ctx_t *ctx, const void *d_block, size_t m,
                       knn_neighbour_t *d_out, void *stream);
 
 /* Diagnostics of the last knn_ctx_end: engine mode (0 integer-exact,
  * 1 fp64 GEMM + exact re-rank, 2 exact scan) and the corpus split count. */
-int knn_ctx_info(const knn_ctx_t *ctx, int *mode, int *splits);
+KNN_API int knn_ctx_info(const knn_ctx_t *ctx, int *mode, int *splits);
 
 /* Kernel timing with HIP events on the launch stream (the timers of
  * serial:70-98 at kernel granularity).  enable = 1 starts recording and
  * zeroes the totals, 0 stops (totals kept), -1 only reads.  Totals (ms) cover every
  * k_dist_topk / k_merge launch since the last reset whose knn_ctx_end has
  * returned; *launches counts k_dist_topk launches. */
-int knn_ctx_profile(knn_ctx_t *ctx, int enable, double *dist_ms, double *merge_ms,
+KNN_API int knn_ctx_profile(knn_ctx_t *ctx, int enable, double *dist_ms, double *merge_ms,
                     int *launches);
 
 #ifdef __cplusplus

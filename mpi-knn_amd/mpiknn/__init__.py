@@ -52,18 +52,13 @@ def _share_torch_runtime():
     """One HIP runtime per process.  PyTorch-ROCm ships its own
     libamdhip64/librccl with the same sonames as /opt/rocm's; if libknn
     pulled in the system copies first, torch would later load a second HIP
-    runtime and find no GPU.  Pre-load torch's copies (by path, without
-    importing torch) so libknn binds to them; without torch the system
-    ROCm libraries are used."""
-    import importlib.util
-    spec = importlib.util.find_spec("torch")
-    if spec is None or not spec.submodule_search_locations:
-        return
-    tlib = os.path.join(list(spec.submodule_search_locations)[0], "lib")
-    for name in ("libamdhip64.so", "librccl.so"):
-        path = os.path.join(tlib, name)
-        if os.path.exists(path):
-            ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    runtime (no GPU found, heap corruption at exit).  Importing torch first
+    (no device is touched) makes libknn bind to torch's copies; without
+    torch the system ROCm libraries are used."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 
 
 def _load():

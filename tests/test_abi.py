@@ -1,0 +1,96 @@
+"""The C-ABI library without a GPU: it loads, exports every entry point
+include/knn.h declares, and its host-only pieces (vote, MAT reader, error
+paths) behave.  No device compute is attempted here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import datasets
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "knn.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(knn_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_every_declared_symbol_exported(knn):
+    names = header_functions()
+    assert len(names) >= 19
+    out = subprocess.check_output(["nm", "-D", "--defined-only", knn.LIB_PATH]).decode()
+    exported = set(re.findall(r" T (knn_\w+)", out))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    assert set(knn.API_SYMBOLS) == set(names)
+
+
+def test_internal_symbols_hidden(knn):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", knn.LIB_PATH]).decode()
+    exported = set(re.findall(r" T (knn_\w+)", out))
+    assert exported == set(header_functions()), sorted(exported - set(header_functions()))
+
+
+def test_strerror(knn):
+    assert knn.strerror(0) == "ok"
+    assert "device" in knn.strerror(knn.ERR_NODEVICE)
+    assert knn.strerror(999) == "unknown status"
+
+
+def test_invalid_arguments(knn):
+    lib = knn.lib
+    out = np.zeros((4, 3), dtype=knn.NB_DTYPE)
+    X = np.ones((4, 2))
+    p = X.ctypes.data_as(ctypes.c_void_p)
+    o = out.ctypes.data_as(ctypes.c_void_p)
+    assert lib.knn_search(None, 4, 2, 1, None, 3, 1, 0, o) == knn.ERR_INVALID
+    assert lib.knn_search(p, 4, 2, 7, None, 3, 1, 0, o) == knn.ERR_INVALID
+    assert lib.knn_search(p, 4, 2, 1, None, 33, 1, 0, o) == knn.ERR_UNSUPPORTED
+    assert lib.knn_search(p, 4, 2, 1, None, 3, 1, 1, o) == knn.ERR_UNSUPPORTED
+    assert lib.knn_search(p, 4, 2, 1, None, 3, 0, 0, o) == knn.ERR_INVALID
+    h = ctypes.c_void_p()
+    assert lib.knn_ctx_create(ctypes.byref(h), 0, 0, 2, 4, 3) == knn.ERR_INVALID
+    assert lib.knn_block_pack(None, 4, 4, 2, None, 4, 0, None) == knn.ERR_INVALID
+
+
+def test_block_layout(knn):
+    # rows padded to 128, features to 16, + norms + 8 meta doubles
+    assert knn.block_bytes(60000, 784) == (60032 * 784 + 60032 + 8) * 8
+    assert knn.block_meta_offset(1, 1) == (128 * 16 + 128) * 8
+
+
+@pytest.mark.parametrize("rule", [0, 1, 2])
+def test_classify_matches_oracle(knn, oracle, rule):
+    X, y = datasets.digits()
+    nb = oracle.knn(X, 30, labels=y)
+    nb2 = nb.view(knn.NB_DTYPE)
+    p_ref, m_ref = oracle.classify(nb, y, 10, rule)
+    p, m = knn.classify(nb2, y, 10, rule)
+    assert m == m_ref and np.array_equal(p, p_ref)
+
+
+def test_classify_empty_slots(knn):
+    # fewer than k neighbours: idx 0 slots are skipped (the reference reads
+    # labels[-1] there)
+    nb = np.zeros((2, 4), dtype=knn.NB_DTYPE)
+    nb["idx"] = [[2, 0, 0, 0], [1, 0, 0, 0]]
+    labels = np.array([3.0, 5.0])
+    pred, m = knn.classify(nb, labels, 10, knn.VOTE_SERIAL)
+    assert list(pred) == [5, 3] and m == 0
+
+
+def test_no_device_reports_cleanly(knn):
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    with pytest.raises(knn.KnnError) as e:
+        knn.search(np.ones((5, 3)), 2)
+    assert e.value.status == knn.ERR_NODEVICE
