@@ -199,12 +199,32 @@ __device__ __forceinline__ void wave_argmin(double &d, int &i)
 // ds_read_b128, and one global_load_lds (1 KiB) stages 16 rows x 64
 // contiguous bytes.  LDS images are lane-linear -> conflict-free reads.
 //
+// Staging is an NST-deep ring of LDS stages filled by global_load_lds: the
+// loads for chunk c+NST-1 are issued right after the barrier of chunk c and
+// stay in flight across NST-2 barriers (counted `s_waitcnt vmcnt`, raw
+// s_barrier -- a __syncthreads() would drain them, guide sec.5
+// 'Pipelining across barriers').  Every wave issues exactly KNN_GLDS loads
+// per chunk so the count is static: 2 corpus pieces, 2 query pieces and a
+// 256-byte slice of the tile's corpus norms (waves 4..7 load a spare copy).
+//
 // LDS (one array, guide 'second __shared__ object' trap):
-//   [0,32K)  C pieces  [buf][mt*2+p][64 lanes][2 doubles]
-//   [32K,64K) Q pieces [buf][w*2+p][64][2]
-//   [64K,66K) corpus norms of the tile, [tile&1][128]
+//   stage s at s*32K: C pieces [mt*2+p][64 lanes][16 B] (16 KiB),
+//                     Q pieces [w*2+p][64][16 B]        (16 KiB)
+//   NST*32K:          corpus norms ring [tile&3][128 doubles]
+//   NST*32K + 4K:     spare norm slices of waves 4..7
 // ---------------------------------------------------------------------------
-template <int KL, int KS>
+#define KNN_GLDS 5
+template <int NST>
+__device__ __forceinline__ void wait_stage(int ahead)
+{
+    // chunks still allowed in flight: min(NST-2, ahead), KNN_GLDS loads each
+    static_assert(NST == 4, "counted waits below assume a 4-stage ring");
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int KL, int KS, int NST, int PIPE>
 __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const double *__restrict__ qblk, const double *__restrict__ qnorm, size_t q_base, int nq,
     const double *__restrict__ cblk, const double *__restrict__ cnorm, size_t c_base, int nc,
@@ -212,7 +232,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T,
     int nq_pad)
 {
-    __shared__ __attribute__((aligned(16))) char smem[66 * 1024];
+    __shared__ __attribute__((aligned(16))) char smem[NST * 32768 + 4096 + 1024];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, j16 = lane & 15;
     const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;
@@ -241,32 +261,77 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     LDS_AS char *lds = (LDS_AS char *)smem;
 
     auto stage = [&](int c) {
-        const int t = t_lo + c / nfc, fc = c % nfc, buf = c & 1;
+        const int t = t_lo + c / nfc, fc = c % nfc, buf = c % NST;
         const int f = KNN_BK * fc + 2 * g;
         const double *csrc = cblk + (size_t)(t * KNN_TC + 16 * wave + j16) * n_pad + f;
         const double *qsrc = qblk + (size_t)(qrow0 + 16 * wave + j16) * n_pad + f;
-        LDS_AS char *cdst = lds + buf * 16384 + wave * 2048;
-        LDS_AS char *qdst = lds + 32768 + buf * 16384 + wave * 2048;
+        LDS_AS char *cdst = lds + buf * 32768 + wave * 2048;
+        LDS_AS char *qdst = lds + buf * 32768 + 16384 + wave * 2048;
         __builtin_amdgcn_global_load_lds((const void *)(csrc), (LDS_AS void *)cdst, 16, 0, 0);
         __builtin_amdgcn_global_load_lds((const void *)(csrc + 8), (LDS_AS void *)(cdst + 1024), 16, 0, 0);
         __builtin_amdgcn_global_load_lds((const void *)(qsrc), (LDS_AS void *)qdst, 16, 0, 0);
         __builtin_amdgcn_global_load_lds((const void *)(qsrc + 8), (LDS_AS void *)(qdst + 1024), 16, 0, 0);
-        if (fc == 0 && wave == 0) {
-            __builtin_amdgcn_global_load_lds((const void *)(cnorm + (size_t)t * KNN_TC + 2 * lane),
-                                             (LDS_AS void *)(lds + 65536 + (t & 1) * 1024), 16, 0, 0);
-        }
+        // norms of tile t: waves 0..3 load 32 doubles each (4 B per lane)
+        const int w4 = wave & 3;
+        LDS_AS char *ndst = (wave < 4) ? lds + NST * 32768 + (t & 3) * 1024 + w4 * 256
+                                       : lds + NST * 32768 + 4096 + w4 * 256;
+        __builtin_amdgcn_global_load_lds((const void *)((const char *)(cnorm + (size_t)t * KNN_TC + 32 * w4) + 4 * lane),
+                                         (LDS_AS void *)ndst, 4, 0, 0);
     };
 
-    if (total > 0) {
-        stage(0);
-        __syncthreads();
-    }
-    for (int c = 0; c < total; c++) {
-        const int buf = c & 1;
-        if (c + 1 < total) stage(c + 1);
-        {
-            const LDS_AS dbl2 *cs = (const LDS_AS dbl2 *)(lds + buf * 16384);
-            const LDS_AS dbl2 *qs = (const LDS_AS dbl2 *)(lds + 32768 + buf * 16384 + wave * 2048);
+    // ---- epilogue of tile t: d^2, threshold filter, insertion ----
+    auto epilogue = [&](int t) {
+        const LDS_AS double *cn = (const LDS_AS double *)(lds + NST * 32768 + (t & 3) * 1024);
+        const double lim = L[KL - 1] < thr ? L[KL - 1] : thr;
+#pragma unroll
+        for (int mt = 0; mt < 8; mt++) {
+            double d[4];
+            int id[4];
+            unsigned pend = 0;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int lrow = 16 * mt + g + 4 * r;
+                const int row = t * KNN_TC + lrow;
+                double v = fma(-2.0, acc[mt][r], qn + cn[lrow]);
+                const bool valid = (row < nc) && ((long)c_base + row != gq) &&
+                                   !(mode == KNN_MODE_INT && v == 0.0);
+                d[r] = valid ? v : KNN_INF;
+                id[r] = (int)(c_base + row);
+                pend |= (d[r] <= lim) ? (1u << r) : 0u;
+            }
+            while (__ballot(pend != 0) != 0ull) {
+                const int b = pend ? __builtin_ctz(pend) : 4;
+                double dd = (b == 0) ? d[0] : (b == 1) ? d[1] : (b == 2) ? d[2] : (b == 3) ? d[3] : KNN_INF;
+                int ii = (b == 0) ? id[0] : (b == 1) ? id[1] : (b == 2) ? id[2] : id[3];
+                pend &= pend - 1;
+                list_insert<KL>(L, I, dd, ii);
+            }
+            acc[mt] = (dbl4){0.0, 0.0, 0.0, 0.0};
+        }
+        // shared threshold of the query's 4 lanes: their union holds
+        // >= KS entries <= max_h L_h[KS/4-1], and every lane already
+        // rejects >= min_h L_h[KL-1]
+        double lmin = L[KL - 1], u = L[KS / 4 - 1];
+        lmin = fmin(lmin, __shfl_xor(lmin, 16));
+        lmin = fmin(lmin, __shfl_xor(lmin, 32));
+        u = fmax(u, __shfl_xor(u, 16));
+        u = fmax(u, __shfl_xor(u, 32));
+        thr = fmin(lmin, u);
+    };
+
+    const int npre = total < NST - 1 ? total : NST - 1;
+    for (int c = 0; c < npre; c++) stage(c);
+
+    if constexpr (PIPE == 0) {
+        // one segment per chunk: barrier, then all 18 fragment reads, then
+        // the chunk's 32 MFMAs
+        for (int c = 0; c < total; c++) {
+            const int buf = c % NST;
+            wait_stage<NST>(total - 1 - c);
+            __builtin_amdgcn_s_barrier();      // chunk c visible; stage (c-1)%NST free
+            if (c + NST - 1 < total) stage(c + NST - 1);
+            const LDS_AS dbl2 *cs = (const LDS_AS dbl2 *)(lds + buf * 32768);
+            const LDS_AS dbl2 *qs = (const LDS_AS dbl2 *)(lds + buf * 32768 + 16384 + wave * 2048);
             dbl2 b0 = qs[lane];
             dbl2 b1 = qs[64 + lane];
 #pragma unroll
@@ -278,48 +343,55 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, b1.x, acc[mt], 0, 0, 0);
                 acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, b1.y, acc[mt], 0, 0, 0);
             }
+            if ((c % nfc) == nfc - 1) epilogue(t_lo + c / nfc);
         }
-        if ((c % nfc) == nfc - 1) {
-            // ---- epilogue for tile t: d^2, threshold filter, insertion ----
-            const int t = t_lo + c / nfc;
-            const LDS_AS double *cn = (const LDS_AS double *)(lds + 65536 + (t & 1) * 1024);
-            const double lim = L[KL - 1] < thr ? L[KL - 1] : thr;
+    } else {
+        // two segments per chunk, fragments one half-chunk ahead:
+        //   A: MFMAs of half 0 of chunk c  || LDS reads of half 1 of chunk c
+        //      lgkmcnt(0); wait chunk c+1; barrier; stage chunk c+NST
+        //   B: MFMAs of half 1 of chunk c  || LDS reads of half 0 of chunk c+1
+        // so the barrier that frees stage c%NST also publishes chunk c+1, and
+        // no segment starts with its operands still in flight.
+        dbl2 fa[8], fb[8];
+        dbl2 ga, gb;
+        auto read_half = [&](int c, int p, dbl2 (&fr)[8], dbl2 &gq_) {
+            const int buf = c % NST;
+            const LDS_AS dbl2 *cs = (const LDS_AS dbl2 *)(lds + buf * 32768);
+            const LDS_AS dbl2 *qs = (const LDS_AS dbl2 *)(lds + buf * 32768 + 16384 + wave * 2048);
+            gq_ = qs[p * 64 + lane];
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) fr[mt] = cs[(mt * 2 + p) * 64 + lane];
+        };
+        auto mfma_half = [&](const dbl2 (&fr)[8], const dbl2 &b) {
 #pragma unroll
             for (int mt = 0; mt < 8; mt++) {
-                double d[4];
-                int id[4];
-                unsigned pend = 0;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int lrow = 16 * mt + g + 4 * r;
-                    const int row = t * KNN_TC + lrow;
-                    double v = fma(-2.0, acc[mt][r], qn + cn[lrow]);
-                    const bool valid = (row < nc) && ((long)c_base + row != gq) &&
-                                       !(mode == KNN_MODE_INT && v == 0.0);
-                    d[r] = valid ? v : KNN_INF;
-                    id[r] = (int)(c_base + row);
-                    pend |= (d[r] <= lim) ? (1u << r) : 0u;
-                }
-                while (__ballot(pend != 0) != 0ull) {
-                    const int b = pend ? __builtin_ctz(pend) : 4;
-                    double dd = (b == 0) ? d[0] : (b == 1) ? d[1] : (b == 2) ? d[2] : (b == 3) ? d[3] : KNN_INF;
-                    int ii = (b == 0) ? id[0] : (b == 1) ? id[1] : (b == 2) ? id[2] : id[3];
-                    pend &= pend - 1;
-                    list_insert<KL>(L, I, dd, ii);
-                }
-                acc[mt] = (dbl4){0.0, 0.0, 0.0, 0.0};
+                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[mt].x, b.x, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[mt].y, b.y, acc[mt], 0, 0, 0);
             }
-            // shared threshold of the query's 4 lanes: their union holds
-            // >= KS entries <= max_h L_h[KS/4-1], and every lane already
-            // rejects >= min_h L_h[KL-1]
-            double lmin = L[KL - 1], u = L[KS / 4 - 1];
-            lmin = fmin(lmin, __shfl_xor(lmin, 16));
-            lmin = fmin(lmin, __shfl_xor(lmin, 32));
-            u = fmax(u, __shfl_xor(u, 16));
-            u = fmax(u, __shfl_xor(u, 32));
-            thr = fmin(lmin, u);
+        };
+        if (total > 0) {
+            wait_stage<NST>(total - 1);
+            __builtin_amdgcn_s_barrier();
+            if (NST - 1 < total) stage(NST - 1);
+            read_half(0, 0, fa, ga);
         }
-        __syncthreads();
+        for (int c = 0; c < total; c++) {
+            read_half(c, 1, fb, gb);
+            mfma_half(fa, ga);
+            __builtin_amdgcn_sched_barrier(0);
+            if (c + 1 < total) {
+                // builtin, not asm: the waitcnt pass must see that fb/gb have
+                // landed, or it re-waits for the reads issued below
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                wait_stage<NST>(total - 2 - c);
+                __builtin_amdgcn_s_barrier();  // chunk c+1 visible; stage c%NST free
+                if (c + NST < total) stage(c + NST);
+                read_half(c + 1, 0, fa, ga);
+            }
+            mfma_half(fb, gb);
+            __builtin_amdgcn_sched_barrier(0);
+            if ((c % nfc) == nfc - 1) epilogue(t_lo + c / nfc);
+        }
     }
 
     if (myq < nq) {
@@ -668,9 +740,22 @@ extern "C" int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_
         return KNN_ERR_INVALID;
     const double *qnorm = qblk + q_rows_pad * np;
     const double *cnorm = cblk + c_rows_pad * np;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP>), dim3((unsigned)(nqb * nsplit)), dim3(512), 0,
-                       (hipStream_t)stream, qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc,
-                       n, np, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad);
+    // KNN_PIPE=0 selects the one-segment main loop (kept for A/B timing)
+    static int pipe = -1;
+    if (pipe < 0) {
+        const char *e = getenv("KNN_PIPE");
+        pipe = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (pipe)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, 4, 1>),
+                           dim3((unsigned)(nqb * nsplit)), dim3(512), 0, (hipStream_t)stream,
+                           qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles,
+                           nsplit, nqb, meta, part_d, part_i, part_T, nq_pad);
+    else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, 4, 0>),
+                           dim3((unsigned)(nqb * nsplit)), dim3(512), 0, (hipStream_t)stream,
+                           qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles,
+                           nsplit, nqb, meta, part_d, part_i, part_T, nq_pad);
     return hip_status();
 }
 

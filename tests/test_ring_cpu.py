@@ -1,0 +1,119 @@
+"""The per-rank ring driver (mpiknn/ring.py) under gloo on CPU.
+
+world_size 2 and 3 processes run the real ring_search() schedule -- meta
+all-reduce, P-1 isend/irecv hops per pass with the query block kept
+resident, the rescan pass -- with a CPU stand-in engine whose per-block fold
+is the oracle's block restatement (test-only; the product engine is HIP).
+Every rank must end with exactly the serial-semantics lists of its rows and
+must have folded every block exactly once per pass.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class CpuEngine:
+    """Same interface as mpiknn.ring.GpuEngine; blocks are (R, n) float64."""
+
+    def __init__(self, oracle, n, R, nq, k, force_rescan):
+        self.O = oracle
+        self.n, self.R, self.nq, self.k = n, R, nq, k
+        self.qb = torch.zeros((R, n + 1), dtype=torch.float64)   # last column: row count
+        self.bufa = torch.zeros_like(self.qb)
+        self.bufb = torch.zeros_like(self.qb)
+        self.meta = torch.zeros(8, dtype=torch.float64)
+        self.force_rescan = force_rescan
+        self.visits = {False: [], True: []}
+
+    def pack(self, src):
+        rows = src.shape[0]
+        self.qb.zero_()
+        self.qb[:rows, : self.n] = src
+        self.qb[0, self.n] = rows
+        self.meta[0] = float(src.abs().max())
+
+    def begin(self, q_base):
+        self.q_base = q_base
+        self.lists = self.O.lists_init(self.nq, self.k)
+
+    def step(self, buf, rows, base, rescan=False):
+        assert int(buf[0, self.n]) == rows           # the block we were told we hold
+        self.visits[rescan].append(base)
+        target = self.rescan_lists if rescan else self.lists
+        self.O.knn_block(self.qb[: self.nq, : self.n].numpy(), self.q_base,
+                         buf[:rows, : self.n].numpy(), base, target)
+
+    def end(self):
+        self.rescan_lists = self.O.lists_init(self.nq, self.k)
+        return 1 if self.force_rescan else 0
+
+    def rescan_end(self):
+        assert np.array_equal(self.rescan_lists, self.lists)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, force_rescan, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(here, "..", "oracle"), os.path.join(here, "..", "mpi-knn_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import datasets
+        import oracle
+        from mpiknn.ring import partition, ring_search
+        X, _ = datasets.digits_real()
+        m, n = X.shape
+        R, blocks = partition(m, world)
+        base, rows = blocks[rank]
+        eng = CpuEngine(oracle, n, R, rows, 30, force_rescan)
+        eng.pack(torch.from_numpy(X[base:base + rows]))
+        ring_search(dist, torch, eng, rank, world, m, base)
+        full = oracle.knn(X, 30, rows=(base, rows))
+        ok = np.array_equal(eng.lists[["distance", "idx"]], full[["distance", "idx"]])
+        every = sorted(eng.visits[False]) == sorted(b for b, _ in blocks)
+        every_rescan = (not force_rescan) or sorted(eng.visits[True]) == sorted(b for b, _ in blocks)
+        meta_ok = float(eng.meta[0]) == float(np.abs(X).max())
+        q.put((rank, ok, every, every_rescan, meta_ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,force_rescan", [(2, False), (3, True)])
+def test_ring_schedule_gloo(world, force_rescan):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, force_rescan, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, every, every_rescan, meta_ok in sorted(res):
+        assert ok, "rank %d lists differ from the serial scan" % rank
+        assert every, "rank %d did not fold every block once" % rank
+        assert every_rescan, "rank %d rescan pass missed a block" % rank
+        assert meta_ok, "rank %d meta not max-reduced" % rank
+
+
+def test_partition_covers_all_rows():
+    from mpiknn.ring import partition
+    for m, P in [(60000, 8), (60000, 7), (10, 3), (9, 3)]:
+        R, blocks = partition(m, P)
+        assert sum(r for _, r in blocks) == m
+        assert all(b == i * R for i, (b, _) in enumerate(blocks))
