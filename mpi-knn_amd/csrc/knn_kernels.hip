@@ -10,7 +10,7 @@
 //                with d^2 = |q|^2 + |c|^2 - 2G and a per-lane register top-k
 //                (insertion network) behind a shared threshold.  One
 //                workgroup = 128 queries x a corpus split; tiles of 128 rows
-//                stream through LDS by global_load_lds, double-buffered.
+//                stream through a 4-stage LDS ring filled by global_load_lds.
 //   k_merge      per query: tournament merge of the split/lane lists with
 //                the running state (ring steps), exact re-rank of new
 //                entries in reference order (GEMM mode).
@@ -191,26 +191,34 @@ __device__ __forceinline__ void wave_argmin(double &d, int &i)
 // f64 MFMA operand map (probed, tools/probe): lane l supplies A[l&15][l>>4]
 // and B[l>>4][l&15]; D reg r of lane l is D[(l>>4)+4r][l&15].  A = corpus
 // rows, B = queries, so lane l ends with 32 d^2 of ONE query (l&15) against
-// corpus rows 16mt + (l>>4) + 4r.  The 4 lanes sharing a query (l>>4 =
-// 0..3) keep separate lists over disjoint row sets; they share a threshold.
+// corpus rows 16mt + (l>>4) + 4r.  The 4 lanes sharing a query (g = l>>4)
+// keep separate lists over disjoint row sets; they share a threshold.
 //
-// k-permutation: in chunk f0, k-step s = 2p+e of lane group g uses feature
-// f0 + 8p + 2g + e, so each lane's two k-steps per piece p are one 16-byte
-// ds_read_b128, and one global_load_lds (1 KiB) stages 16 rows x 64
-// contiguous bytes.  LDS images are lane-linear -> conflict-free reads.
+// k-permutation: in a 16-feature chunk, k-step s = 2p+e of lane group g uses
+// feature 8p + 2g + e, so each lane's two k-steps of piece p are one 16-byte
+// slot (segment 4p+g of the row's 128 bytes): one ds_read_b128.
 //
-// Staging is an NST-deep ring of LDS stages filled by global_load_lds: the
-// loads for chunk c+NST-1 are issued right after the barrier of chunk c and
-// stay in flight across NST-2 barriers (counted `s_waitcnt vmcnt`, raw
-// s_barrier -- a __syncthreads() would drain them, guide sec.5
-// 'Pipelining across barriers').  Every wave issues exactly KNN_GLDS loads
-// per chunk so the count is static: 2 corpus pieces, 2 query pieces and a
-// 256-byte slice of the tile's corpus norms (waves 4..7 load a spare copy).
+// Staging: an NST-deep ring of LDS stages filled by global_load_lds.  One
+// load instruction moves 8 rows x 128 contiguous bytes (full lines: lane
+// 8r+s fetches 16-byte segment s^(r&7) of row r), so a 16-row block is two
+// loads and its LDS image is [row][segment ^ (row&7)] -- the XOR keeps the
+// fragment reads conflict-free (each ds_read_b128 lane group hits 16
+// distinct 16-byte slots).  The loads for chunk c+NST issue between the
+// MFMAs of chunk c's last segment and stay in flight across NST-2 barriers
+// (counted `s_waitcnt vmcnt`, raw s_barrier; guide sec.5 'Pipelining across
+// barriers').  Each wave issues exactly KNN_GLDS loads per chunk: its
+// m-tile (2), its 16 queries (2), and a 256-byte slice of the tile's norms
+// (waves 4..7 load a spare copy), so the waits are static.
+//
+// Main loop, 4 segments per chunk, each 8 MFMAs interleaved (sched_barrier
+// pinned) with the LDS reads of the next segment's fragments:
+//   S0 (p0, mt0-3) S1 (p0, mt4-7) S2 (p1, mt0-3) | lgkmcnt(0), wait chunk
+//   c+1, barrier | S3 (p1, mt4-7).  The 5 staging loads of chunk c+NST
+//   (into the stage the barrier freed) ride in S3(c) and S0-S2(c+1).
 //
 // LDS (one array, guide 'second __shared__ object' trap):
-//   stage s at s*32K: C pieces [mt*2+p][64 lanes][16 B] (16 KiB),
-//                     Q pieces [w*2+p][64][16 B]        (16 KiB)
-//   NST*32K:          corpus norms ring [tile&3][128 doubles]
+//   stage s at s*32K: C [mt][row 16][128 B] (16 KiB), Q [w][row 16][128 B]
+//   NST*32K:          corpus norms ring [tile&3][g][32] (row 4k+g at [g][k])
 //   NST*32K + 4K:     spare norm slices of waves 4..7
 // ---------------------------------------------------------------------------
 #define KNN_GLDS 5
@@ -224,7 +232,10 @@ __device__ __forceinline__ void wait_stage(int ahead)
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int KL, int KS, int NST, int PIPE>
+// EPI = 0 / ABL != 0 exist only for the tuning harness (tools/probe/kbench):
+// EPI 0 skips the top-k insertion; ABL bit 0 drops the staging loads, bit 1
+// the chunk barrier.  libknn instantiates <.., 1, 0>.
+template <int KL, int KS, int NST, int EPI = 1, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const double *__restrict__ qblk, const double *__restrict__ qnorm, size_t q_base, int nq,
     const double *__restrict__ cblk, const double *__restrict__ cnorm, size_t c_base, int nc,
@@ -257,57 +268,114 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
 #pragma unroll
     for (int mt = 0; mt < 8; mt++) acc[mt] = (dbl4){0.0, 0.0, 0.0, 0.0};
 
-    // wave-uniform LDS bases
     LDS_AS char *lds = (LDS_AS char *)smem;
 
-    auto stage = [&](int c) {
-        const int t = t_lo + c / nfc, fc = c % nfc, buf = c % NST;
-        const int f = KNN_BK * fc + 2 * g;
-        const double *csrc = cblk + (size_t)(t * KNN_TC + 16 * wave + j16) * n_pad + f;
-        const double *qsrc = qblk + (size_t)(qrow0 + 16 * wave + j16) * n_pad + f;
-        LDS_AS char *cdst = lds + buf * 32768 + wave * 2048;
-        LDS_AS char *qdst = lds + buf * 32768 + 16384 + wave * 2048;
-        __builtin_amdgcn_global_load_lds((const void *)(csrc), (LDS_AS void *)cdst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void *)(csrc + 8), (LDS_AS void *)(cdst + 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void *)(qsrc), (LDS_AS void *)qdst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void *)(qsrc + 8), (LDS_AS void *)(qdst + 1024), 16, 0, 0);
-        // norms of tile t: waves 0..3 load 32 doubles each (4 B per lane)
-        const int w4 = wave & 3;
-        LDS_AS char *ndst = (wave < 4) ? lds + NST * 32768 + (t & 3) * 1024 + w4 * 256
-                                       : lds + NST * 32768 + 4096 + w4 * 256;
-        __builtin_amdgcn_global_load_lds((const void *)((const char *)(cnorm + (size_t)t * KNN_TC + 32 * w4) + 4 * lane),
-                                         (LDS_AS void *)ndst, 4, 0, 0);
+    // ---- staging cursor -------------------------------------------------
+    // load i of a chunk: i = 0,1 -> rows 8i..8i+7 of the wave's m-tile,
+    // i = 2,3 -> of its 16 queries, i = 4 -> norm slice.  Lane 8r+s reads
+    // segment s^(r&7) of row r: per-lane offsets are fixed, the chunk moves
+    // a wave-uniform base.
+    const int lr = lane >> 3, ls = lane & 7;
+    const int seg_off = 2 * (ls ^ lr);                       // doubles within the 128-B row
+    const int lane_c = (16 * wave + lr) * n_pad + seg_off;   // corpus row 16w+lr of a tile
+    const double *const qbase = qblk + (size_t)(qrow0 + 16 * wave + lr) * n_pad + seg_off;
+    // norms land permuted as [g][k] = norm of row 4k+g (4-byte pieces)
+    const int cn_unit = (wave & 3) * 64 + lane;              // 4-byte unit 0..255
+    const int cn_p = cn_unit >> 1;
+    const int cn_src_off = ((cn_p & 31) * 4 + (cn_p >> 5)) * 8 + (cn_unit & 1) * 4;
+    int s_c = 0, s_t = t_lo, s_fc = 0;                       // next chunk to stage
+    auto glds1 = [&](int i) {
+        if constexpr ((ABL & 1) != 0) return;
+        LDS_AS char *dst = lds + (s_c & (NST - 1)) * 32768 + wave * 2048;
+        const size_t fo = (size_t)KNN_BK * s_fc;
+        const double *csrc = cblk + (size_t)s_t * KNN_TC * n_pad + fo + lane_c;
+        const double *qsrc = qbase + fo;
+        if (i == 0) __builtin_amdgcn_global_load_lds((const void *)csrc, (LDS_AS void *)dst, 16, 0, 0);
+        if (i == 1) __builtin_amdgcn_global_load_lds((const void *)(csrc + 8 * (size_t)n_pad),
+                                                     (LDS_AS void *)(dst + 1024), 16, 0, 0);
+        if (i == 2) __builtin_amdgcn_global_load_lds((const void *)qsrc, (LDS_AS void *)(dst + 16384), 16, 0, 0);
+        if (i == 3) __builtin_amdgcn_global_load_lds((const void *)(qsrc + 8 * (size_t)n_pad),
+                                                     (LDS_AS void *)(dst + 17408), 16, 0, 0);
+        if (i == 4) {
+            LDS_AS char *ndst = (wave < 4) ? lds + NST * 32768 + (s_t & 3) * 1024 + (wave & 3) * 256
+                                           : lds + NST * 32768 + 4096 + (wave & 3) * 256;
+            __builtin_amdgcn_global_load_lds(
+                (const void *)((const char *)(cnorm + (size_t)s_t * KNN_TC) + cn_src_off),
+                (LDS_AS void *)ndst, 4, 0, 0);
+        }
+    };
+    auto advance = [&]() {
+        s_c++;
+        if (++s_fc == nfc) {
+            s_fc = 0;
+            s_t++;
+        }
     };
 
-    // ---- epilogue of tile t: d^2, threshold filter, insertion ----
+    // ---- epilogue of tile t: d^2, threshold filter, insertion ------------
     auto epilogue = [&](int t) {
-        const LDS_AS double *cn = (const LDS_AS double *)(lds + NST * 32768 + (t & 3) * 1024);
+        const LDS_AS double *cng = (const LDS_AS double *)(lds + NST * 32768 + (t & 3) * 1024) + 32 * g;
         const double lim = L[KL - 1] < thr ? L[KL - 1] : thr;
+        // INT mode: d^2 is exact and >= 0, so "S != 0" (serial:86) is d^2 > 0
+        const double zfloor = (mode == KNN_MODE_INT) ? 0.0 : -KNN_INF;
+        // wave-uniform: only the block's last tile has rows >= nc, and only
+        // tiles holding one of this wave's queries contain a self pair
+        const int row0 = t * KNN_TC;
+        const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 16 * wave;
+        const bool masked = (row0 + KNN_TC > nc) || (gw0 < gt0 + KNN_TC && gt0 < gw0 + 16);
+        // d^2 overwrites the accumulators in place (no extra registers)
+        unsigned pend_all = 0;
 #pragma unroll
         for (int mt = 0; mt < 8; mt++) {
-            double d[4];
-            int id[4];
-            unsigned pend = 0;
+            const dbl2 n01 = ((const LDS_AS dbl2 *)cng)[2 * mt];
+            const dbl2 n23 = ((const LDS_AS dbl2 *)cng)[2 * mt + 1];
+            const double cnr[4] = {n01.x, n01.y, n23.x, n23.y};
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int lrow = 16 * mt + g + 4 * r;
-                const int row = t * KNN_TC + lrow;
-                double v = fma(-2.0, acc[mt][r], qn + cn[lrow]);
-                const bool valid = (row < nc) && ((long)c_base + row != gq) &&
-                                   !(mode == KNN_MODE_INT && v == 0.0);
-                d[r] = valid ? v : KNN_INF;
-                id[r] = (int)(c_base + row);
-                pend |= (d[r] <= lim) ? (1u << r) : 0u;
+                double v = fma(-2.0, acc[mt][r], qn + cnr[r]);
+                if (masked) {
+                    const int row = row0 + 16 * mt + g + 4 * r;
+                    v = (row < nc && (long)c_base + row != gq) ? v : KNN_INF;
+                }
+                acc[mt][r] = v;
+                pend_all |= (v <= lim && v > zfloor) ? (1u << (4 * mt + r)) : 0u;
             }
-            while (__ballot(pend != 0) != 0ull) {
-                const int b = pend ? __builtin_ctz(pend) : 4;
-                double dd = (b == 0) ? d[0] : (b == 1) ? d[1] : (b == 2) ? d[2] : (b == 3) ? d[3] : KNN_INF;
-                int ii = (b == 0) ? id[0] : (b == 1) ? id[1] : (b == 2) ? id[2] : id[3];
-                pend &= pend - 1;
+        }
+        if constexpr (EPI == 0) {
+            double s = acc[0][0];
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++)
+                s = fmin(s, fmin(fmin(acc[mt][0], acc[mt][1]), fmin(acc[mt][2], acc[mt][3])));
+            L[0] = fmin(L[0], s);
+            pend_all = 0;
+        }
+        const bool any = __ballot(pend_all != 0) != 0ull;   // rare late in the scan
+        if (any) {
+            // one wave round per survivor of the busiest lane: each lane
+            // takes its lowest pending candidate (= lowest row: the stable
+            // tie order) through a 5-level select tree over the 32 d^2
+            while (__ballot(pend_all != 0) != 0ull) {
+                const int b = pend_all ? __builtin_ctz(pend_all) : 0;
+                const bool b0 = b & 1, b1 = b & 2, b2 = b & 4, b3 = b & 8, b4 = b & 16;
+                double v[8];
+#pragma unroll
+                for (int mt = 0; mt < 8; mt++) {
+                    const double lo = b0 ? acc[mt][1] : acc[mt][0];
+                    const double hi = b0 ? acc[mt][3] : acc[mt][2];
+                    v[mt] = b1 ? hi : lo;
+                }
+                const double w0 = b2 ? v[1] : v[0], w1 = b2 ? v[3] : v[2];
+                const double w2 = b2 ? v[5] : v[4], w3 = b2 ? v[7] : v[6];
+                const double x0 = b3 ? w1 : w0, x1 = b3 ? w3 : w2;
+                const double dd = pend_all ? (b4 ? x1 : x0) : KNN_INF;
+                const int ii = (int)(c_base + row0 + 16 * (b >> 2) + g + 4 * (b & 3));
+                pend_all &= pend_all - 1;
                 list_insert<KL>(L, I, dd, ii);
             }
-            acc[mt] = (dbl4){0.0, 0.0, 0.0, 0.0};
         }
+#pragma unroll
+        for (int mt = 0; mt < 8; mt++) acc[mt] = (dbl4){0.0, 0.0, 0.0, 0.0};
+        if (!any) return;
         // shared threshold of the query's 4 lanes: their union holds
         // >= KS entries <= max_h L_h[KS/4-1], and every lane already
         // rejects >= min_h L_h[KL-1]
@@ -319,78 +387,98 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         thr = fmin(lmin, u);
     };
 
-    const int npre = total < NST - 1 ? total : NST - 1;
-    for (int c = 0; c < npre; c++) stage(c);
+    // ---- fragments: quarter (p, h) = m-tiles 4h..4h+3 of piece p ---------
+    auto cs_of = [&](int c) { return lds + (c & (NST - 1)) * 32768; };
+    // 16-byte slot of (row, segment 4p+g) in a 16-row image
+    const int fslot = j16 * 128 + 16 * ((4 * 0 + g) ^ (j16 & 7));
+    const int fslot1 = j16 * 128 + 16 * ((4 * 1 + g) ^ (j16 & 7));
+    dbl2 f0[4], f1[4];
+    dbl2 b0, b1;
+    auto rd = [&](LDS_AS char *st, int p, int h, dbl2 (&f)[4], int j) {
+        f[j] = *(const LDS_AS dbl2 *)(st + (4 * h + j) * 2048 + (p ? fslot1 : fslot));
+    };
+    auto rdq = [&](LDS_AS char *st, int p) {
+        return *(const LDS_AS dbl2 *)(st + 16384 + wave * 2048 + (p ? fslot1 : fslot));
+    };
+    auto mm = [&](const dbl2 (&f)[4], const dbl2 &b, int h, int j) {
+        acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].x, b.x, acc[4 * h + j], 0, 0, 0);
+        acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].y, b.y, acc[4 * h + j], 0, 0, 0);
+    };
 
-    if constexpr (PIPE == 0) {
-        // one segment per chunk: barrier, then all 18 fragment reads, then
-        // the chunk's 32 MFMAs
-        for (int c = 0; c < total; c++) {
-            const int buf = c % NST;
-            wait_stage<NST>(total - 1 - c);
-            __builtin_amdgcn_s_barrier();      // chunk c visible; stage (c-1)%NST free
-            if (c + NST - 1 < total) stage(c + NST - 1);
-            const LDS_AS dbl2 *cs = (const LDS_AS dbl2 *)(lds + buf * 32768);
-            const LDS_AS dbl2 *qs = (const LDS_AS dbl2 *)(lds + buf * 32768 + 16384 + wave * 2048);
-            dbl2 b0 = qs[lane];
-            dbl2 b1 = qs[64 + lane];
+    // prologue: every stage is free, fill all NST of them
+    const int npre = total < NST ? total : NST;
+    for (int c = 0; c < npre; c++) {
 #pragma unroll
-            for (int mt = 0; mt < 8; mt++) {
-                dbl2 a0 = cs[(mt * 2) * 64 + lane];
-                dbl2 a1 = cs[(mt * 2 + 1) * 64 + lane];
-                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, b0.x, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, b0.y, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, b1.x, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, b1.y, acc[mt], 0, 0, 0);
-            }
-            if ((c % nfc) == nfc - 1) epilogue(t_lo + c / nfc);
-        }
-    } else {
-        // two segments per chunk, fragments one half-chunk ahead:
-        //   A: MFMAs of half 0 of chunk c  || LDS reads of half 1 of chunk c
-        //      lgkmcnt(0); wait chunk c+1; barrier; stage chunk c+NST
-        //   B: MFMAs of half 1 of chunk c  || LDS reads of half 0 of chunk c+1
-        // so the barrier that frees stage c%NST also publishes chunk c+1, and
-        // no segment starts with its operands still in flight.
-        dbl2 fa[8], fb[8];
-        dbl2 ga, gb;
-        auto read_half = [&](int c, int p, dbl2 (&fr)[8], dbl2 &gq_) {
-            const int buf = c % NST;
-            const LDS_AS dbl2 *cs = (const LDS_AS dbl2 *)(lds + buf * 32768);
-            const LDS_AS dbl2 *qs = (const LDS_AS dbl2 *)(lds + buf * 32768 + 16384 + wave * 2048);
-            gq_ = qs[p * 64 + lane];
+        for (int i = 0; i < KNN_GLDS; i++) glds1(i);
+        advance();
+    }
+    // a chunk's staging loads are spread over S3 of one chunk and S0-S2 of
+    // the next (all after the barrier that freed its stage)
+    bool spread = false;
+    if (total > 0) {
+        if (total > 3) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+        else wait_stage<NST>(total - 1);
+        __builtin_amdgcn_s_barrier();
+        b0 = rdq(cs_of(0), 0);
 #pragma unroll
-            for (int mt = 0; mt < 8; mt++) fr[mt] = cs[(mt * 2 + p) * 64 + lane];
-        };
-        auto mfma_half = [&](const dbl2 (&fr)[8], const dbl2 &b) {
+        for (int j = 0; j < 4; j++) rd(cs_of(0), 0, 0, f0, j);
+    }
+    int fc_cur = 0;
+    for (int c = 0; c < total; c++) {
+        LDS_AS char *cs = cs_of(c);
+        // S0: (p0, mt0-3) on f0 || read (p0, mt4-7) into f1 [+ staging load 2]
 #pragma unroll
-            for (int mt = 0; mt < 8; mt++) {
-                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[mt].x, b.x, acc[mt], 0, 0, 0);
-                acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[mt].y, b.y, acc[mt], 0, 0, 0);
-            }
-        };
-        if (total > 0) {
-            wait_stage<NST>(total - 1);
-            __builtin_amdgcn_s_barrier();
-            if (NST - 1 < total) stage(NST - 1);
-            read_half(0, 0, fa, ga);
-        }
-        for (int c = 0; c < total; c++) {
-            read_half(c, 1, fb, gb);
-            mfma_half(fa, ga);
+        for (int j = 0; j < 4; j++) {
+            rd(cs, 0, 1, f1, j);
+            if (j == 0 && spread) glds1(2);
+            mm(f0, b0, 0, j);
             __builtin_amdgcn_sched_barrier(0);
-            if (c + 1 < total) {
-                // builtin, not asm: the waitcnt pass must see that fb/gb have
-                // landed, or it re-waits for the reads issued below
-                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-                wait_stage<NST>(total - 2 - c);
-                __builtin_amdgcn_s_barrier();  // chunk c+1 visible; stage c%NST free
-                if (c + NST < total) stage(c + NST);
-                read_half(c + 1, 0, fa, ga);
-            }
-            mfma_half(fb, gb);
+        }
+        // S1: (p0, mt4-7) on f1 || read (p1, mt0-3) + B p1 [+ staging load 3]
+        b1 = rdq(cs, 1);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            rd(cs, 1, 0, f0, j);
+            if (j == 0 && spread) glds1(3);
+            mm(f1, b0, 1, j);
             __builtin_amdgcn_sched_barrier(0);
-            if ((c % nfc) == nfc - 1) epilogue(t_lo + c / nfc);
+        }
+        // S2: (p1, mt0-3) on f0 || read (p1, mt4-7) into f1 [+ staging load 4]
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            rd(cs, 1, 1, f1, j);
+            if (j == 0 && spread) glds1(4);
+            mm(f0, b1, 0, j);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (spread) {
+            advance();
+            spread = false;
+        }
+        if (c + 1 < total) {
+            if constexpr ((ABL & 2) == 0) {
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): f1/b1 landed (builtin:
+                wait_stage<NST>(total - 2 - c);       //  the waitcnt pass must see it)
+                __builtin_amdgcn_s_barrier();         // chunk c+1 visible; stage c%NST free
+            }
+            spread = s_c < total;                     // stage chunk s_c into stage c%NST
+            LDS_AS char *cs1 = cs_of(c + 1);
+            b0 = rdq(cs1, 0);
+            // S3: (p1, mt4-7) on f1 || read (p0, mt0-3) of c+1 [+ staging loads 0, 1]
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                rd(cs1, 0, 0, f0, j);
+                if (j < 2 && spread) glds1(j);
+                mm(f1, b1, 1, j);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) mm(f1, b1, 1, j);
+        }
+        if (++fc_cur == nfc) {
+            fc_cur = 0;
+            epilogue(t_lo + c / nfc);
         }
     }
 
@@ -740,22 +828,10 @@ extern "C" int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_
         return KNN_ERR_INVALID;
     const double *qnorm = qblk + q_rows_pad * np;
     const double *cnorm = cblk + c_rows_pad * np;
-    // KNN_PIPE=0 selects the one-segment main loop (kept for A/B timing)
-    static int pipe = -1;
-    if (pipe < 0) {
-        const char *e = getenv("KNN_PIPE");
-        pipe = (e && e[0] == '0') ? 0 : 1;
-    }
-    if (pipe)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, 4, 1>),
-                           dim3((unsigned)(nqb * nsplit)), dim3(512), 0, (hipStream_t)stream,
-                           qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles,
-                           nsplit, nqb, meta, part_d, part_i, part_T, nq_pad);
-    else
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, 4, 0>),
-                           dim3((unsigned)(nqb * nsplit)), dim3(512), 0, (hipStream_t)stream,
-                           qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles,
-                           nsplit, nqb, meta, part_d, part_i, part_T, nq_pad);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, 4>),
+                       dim3((unsigned)(nqb * nsplit)), dim3(512), 0, (hipStream_t)stream,
+                       qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles,
+                       nsplit, nqb, meta, part_d, part_i, part_T, nq_pad);
     return hip_status();
 }
 
