@@ -213,23 +213,49 @@ __device__ __forceinline__ void wave_argmin(double &d, int &i)
 // Main loop, 4 segments per chunk, each 8 MFMAs interleaved (sched_barrier
 // pinned) with the LDS reads of the next segment's fragments:
 //   S0 (p0, mt0-3) S1 (p0, mt4-7) S2 (p1, mt0-3) | lgkmcnt(0), wait chunk
-//   c+1, barrier | S3 (p1, mt4-7).  The 5 staging loads of chunk c+NST
+//   c+1, barrier | S3 (p1, mt4-7).  The staging loads of chunk c+NST
 //   (into the stage the barrier freed) ride in S3(c) and S0-S2(c+1).
+//
+// Loads per chunk and wave: 4 (corpus rows 2, queries 2), plus one 256-byte
+// norm slice on a tile's first chunk for waves 0..3 -- so the number a wave
+// may leave in flight is known per chunk and waited for exactly.
 //
 // LDS (one array, guide 'second __shared__ object' trap):
 //   stage s at s*32K: C [mt][row 16][128 B] (16 KiB), Q [w][row 16][128 B]
-//   NST*32K:          corpus norms ring [tile&3][g][32] (row 4k+g at [g][k])
-//   NST*32K + 4K:     spare norm slices of waves 4..7
+//   NST*32K:          corpus norms ring [tile&7][g][32] (row 4k+g at [g][k])
 // ---------------------------------------------------------------------------
 #define KNN_GLDS 5
-template <int NST>
-__device__ __forceinline__ void wait_stage(int ahead)
+// chunk c+1 landed when at most 4*min(2, ahead) of this wave's loads remain
+// (a chunk's 5th load, a norm slice, only makes the wait conservative)
+__device__ __forceinline__ void wait_stage4(int ahead)
 {
-    // chunks still allowed in flight: min(NST-2, ahead), KNN_GLDS loads each
-    static_assert(NST == 4, "counted waits below assume a 4-stage ring");
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// s_waitcnt vmcnt(N) for a wave-uniform N in 0..15 (the count is an
+// immediate; waits on the wave's own loads only)
+__device__ __forceinline__ void wait_vm(int N)
+{
+    switch (N) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
 }
 
 // EPI = 0 / ABL != 0 exist only for the tuning harness (tools/probe/kbench):
@@ -243,9 +269,12 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T,
     int nq_pad)
 {
-    __shared__ __attribute__((aligned(16))) char smem[NST * 32768 + 4096 + 1024];
+    __shared__ __attribute__((aligned(16))) char smem[NST * 32768 + 8192];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, j16 = lane & 15;
+    // split-major order: the first resident wave of workgroups shares one
+    // corpus split, so its tiles are read from L2 by every XCD's workgroups
+    // (an XCD-grouped (qb, split) order measured no better: FETCH unchanged)
     const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;
     const int t_lo = (int)((long)split * ntiles / nsplit);
     const int t_hi = (int)((long)(split + 1) * ntiles / nsplit);
@@ -286,6 +315,8 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     int s_c = 0, s_t = t_lo, s_fc = 0;                       // next chunk to stage
     auto glds1 = [&](int i) {
         if constexpr ((ABL & 1) != 0) return;
+        if constexpr ((ABL & 4) != 0) { if (i == 2 || i == 3) return; }   // no query loads
+        if constexpr ((ABL & 8) != 0) { if (i < 2) return; }              // no corpus loads
         LDS_AS char *dst = lds + (s_c & (NST - 1)) * 32768 + wave * 2048;
         const size_t fo = (size_t)KNN_BK * s_fc;
         const double *csrc = cblk + (size_t)s_t * KNN_TC * n_pad + fo + lane_c;
@@ -296,9 +327,8 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         if (i == 2) __builtin_amdgcn_global_load_lds((const void *)qsrc, (LDS_AS void *)(dst + 16384), 16, 0, 0);
         if (i == 3) __builtin_amdgcn_global_load_lds((const void *)(qsrc + 8 * (size_t)n_pad),
                                                      (LDS_AS void *)(dst + 17408), 16, 0, 0);
-        if (i == 4) {
-            LDS_AS char *ndst = (wave < 4) ? lds + NST * 32768 + (s_t & 3) * 1024 + (wave & 3) * 256
-                                           : lds + NST * 32768 + 4096 + (wave & 3) * 256;
+        if (i == 4 && s_fc == 0 && wave < 4) {
+            LDS_AS char *ndst = lds + NST * 32768 + (s_t & 7) * 1024 + wave * 256;
             __builtin_amdgcn_global_load_lds(
                 (const void *)((const char *)(cnorm + (size_t)s_t * KNN_TC) + cn_src_off),
                 (LDS_AS void *)ndst, 4, 0, 0);
@@ -311,10 +341,17 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             s_t++;
         }
     };
+    // staging loads this wave issues for chunk x whose feature chunk is fcx
+    // (0 if x is not staged); fcx comes from counters, never a division
+    auto nloads = [&](int x, int fcx) -> int {
+        if constexpr ((ABL & 1) != 0) return 0;
+        return x < total ? 4 + ((fcx == 0 && wave < 4) ? 1 : 0) : 0;
+    };
+    auto wrap = [&](int f) { return f >= nfc ? f - nfc : f; };   // f < 2*nfc
 
     // ---- epilogue of tile t: d^2, threshold filter, insertion ------------
     auto epilogue = [&](int t) {
-        const LDS_AS double *cng = (const LDS_AS double *)(lds + NST * 32768 + (t & 3) * 1024) + 32 * g;
+        const LDS_AS double *cng = (const LDS_AS double *)(lds + NST * 32768 + (t & 7) * 1024) + 32 * g;
         const double lim = L[KL - 1] < thr ? L[KL - 1] : thr;
         // INT mode: d^2 is exact and >= 0, so "S != 0" (serial:86) is d^2 > 0
         const double zfloor = (mode == KNN_MODE_INT) ? 0.0 : -KNN_INF;
@@ -416,8 +453,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // the next (all after the barrier that freed its stage)
     bool spread = false;
     if (total > 0) {
-        if (total > 3) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
-        else wait_stage<NST>(total - 1);
+        wait_vm(nloads(1, 1 % nfc) + nloads(2, 2 % nfc) + nloads(3, 3 % nfc));   // chunk 0 landed
         __builtin_amdgcn_s_barrier();
         b0 = rdq(cs_of(0), 0);
 #pragma unroll
@@ -458,7 +494,9 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         if (c + 1 < total) {
             if constexpr ((ABL & 2) == 0) {
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): f1/b1 landed (builtin:
-                wait_stage<NST>(total - 2 - c);       //  the waitcnt pass must see it)
+                // chunks c+2, c+3 may stay in flight: 4 loads each (+1 norm
+                // slice on a tile's first chunk, then this waits one early)
+                wait_stage4(total - 2 - c);           //  the waitcnt pass must see it)
                 __builtin_amdgcn_s_barrier();         // chunk c+1 visible; stage c%NST free
             }
             spread = s_c < total;                     // stage chunk s_c into stage c%NST

@@ -78,15 +78,14 @@ int main(int argc, char** argv)
     CK(hipMalloc(&pT, (size_t)15 * nq_pad * 8));
     const double flop = 2.0 * m * (double)m * n;
     for (int rep = 0; rep < 2; rep++) {
-        for (int s : {6, 3}) {
-            float p2 = run<1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-            float p2n = run<0>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-            float a1 = run<0, 1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-            float a2 = run<0, 2>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-            float a3 = run<0, 3>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-            printf("splits %d: full %.2f ms (%.1f TF) | noEPI %.2f  no-glds %.2f  no-sync %.2f  neither %.2f\n",
-                   s, p2, flop / p2 / 1e9, p2n, a1, a2, a3);
-        }
+        const int s = 6;
+        float p2 = run<1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
+        float p2n = run<0>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
+        float a1 = run<0, 1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
+        float a4 = run<0, 4>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
+        float a8 = run<0, 8>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
+        printf("full %.2f ms (%.1f TF) | noEPI %.2f  no-glds %.2f  no-query-glds %.2f  no-corpus-glds %.2f\n",
+               p2, flop / p2 / 1e9, p2n, a1, a4, a8);
     }
     return 0;
 }
