@@ -371,7 +371,9 @@ int knn_search(const double *X, size_t m, size_t n, int layout, const double *la
     if (layout != KNN_COLMAJOR && layout != KNN_ROWMAJOR) return KNN_ERR_INVALID;
     if (ngpus < 1) return KNN_ERR_INVALID;
     int rc = KNN_OK;
-    if (ngpus > 1) {
+    /* KNN_FORCE_RING=1 runs the RCCL ring driver even on one GPU (tests) */
+    const char *force = getenv("KNN_FORCE_RING");
+    if (ngpus > 1 || (force && force[0] == '1')) {
         rc = knn_search_ring_host(X, m, n, layout, k, ngpus, out, &g_last_search_s);
     } else {
         knn_ctx_t *ctx = NULL;

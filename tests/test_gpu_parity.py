@@ -148,3 +148,16 @@ def test_ring_blocks_match_single_device(knn, oracle):
                     e.rescan_end()
                 got = e.result()
                 assert_same(got, full[base:base + rows], "ring P=%d rank %d" % (P, g))
+
+
+def test_rccl_ring_driver_one_gpu(knn, oracle, monkeypatch):
+    """knn_ring.c (ncclCommInitAll, meta ncclAllReduce, ring passes) on the
+    GPUs present; with KNN_FORCE_RING=1 it runs even for one GPU."""
+    import torch
+    ng = torch.cuda.device_count()
+    monkeypatch.setenv("KNN_FORCE_RING", "1")
+    for X in (datasets.mnist_like(1500, 784, seed=4)[0], datasets.digits_real()[0]):
+        ref = oracle.knn(X, 30)
+        for p in sorted({1, ng}):
+            got, _ = knn.search(X, 30, ngpus=p, layout="col")
+            assert_same(got, ref, "rccl ring P=%d" % p)
