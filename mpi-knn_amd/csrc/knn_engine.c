@@ -37,6 +37,8 @@ struct knn_ctx {
     double *part_d;
     int *part_i;
     double *part_T;
+    /* per-query filter bound shared by all splits and ring steps */
+    double *qthr;
     /* running state per query: KNN_KP x (approx d^2, exact S, idx), T pair */
     double *st_d, *st_x, *st_T;
     int *st_i;
@@ -109,6 +111,7 @@ static void ctx_free_buffers(knn_ctx_t *c)
     hipFree(c->part_d);
     hipFree(c->part_i);
     hipFree(c->part_T);
+    hipFree(c->qthr);
     hipFree(c->st_d);
     hipFree(c->st_x);
     hipFree(c->st_T);
@@ -189,6 +192,7 @@ int knn_ctx_create(knn_ctx_t **out, int device, size_t nq, size_t n, size_t bloc
     ok &= hipMalloc((void **)&c->part_d, npart * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->part_i, npart * sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->part_T, (size_t)KNN_MAX_SPLITS * np * sizeof(double)) == hipSuccess;
+    ok &= hipMalloc((void **)&c->qthr, np * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->st_d, np * KNN_KP * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->st_x, np * KNN_KP * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->st_i, np * KNN_KP * sizeof(int)) == hipSuccess;
@@ -234,6 +238,7 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
     c->first_step = 1;
     c->nfail = 0;
     HIPCHK(hipMemsetAsync(c->fail_count, 0, sizeof(int), (hipStream_t)stream));
+    RCHK(knn_launch_fill_inf(c->qthr, (int)c->nq_pad, stream));
     return KNN_OK;
 }
 
@@ -277,7 +282,7 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     }
     RCHK(knn_launch_dist_topk(c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
-                              c->part_d, c->part_i, c->part_T, (int)c->nq_pad, stream));
+                              c->part_d, c->part_i, c->part_T, (int)c->nq_pad, c->qthr, stream));
     if (ev) HIPCHK(hipEventRecord(ev[1], (hipStream_t)stream));
     RCHK(knn_launch_merge(c->part_d, c->part_i, c->part_T, nsplit, (int)c->nq, (int)c->nq_pad,
                           c->first_step, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, cblk,

@@ -41,7 +41,8 @@ int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_t q_base, i
                          const double *cblk, size_t c_rows_pad, size_t c_base, int nc,
                          int n, const double *meta, int nsplit,
                          double *part_d, int *part_i, double *part_T, int nq_pad,
-                         void *stream);
+                         double *qthr, void *stream);
+int knn_launch_fill_inf(double *p, int count, void *stream);
 int knn_launch_merge(const double *part_d, const int *part_i, const double *part_T,
                      int nsplit, int nq, int nq_pad, int first_step,
                      double *st_d, double *st_x, int *st_i, double *st_T,

@@ -198,83 +198,109 @@ __device__ __forceinline__ void wave_argmin(double &d, int &i)
 // feature 8p + 2g + e, so each lane's two k-steps of piece p are one 16-byte
 // slot (segment 4p+g of the row's 128 bytes): one ds_read_b128.
 //
-// Staging: an NST-deep ring of LDS stages filled by global_load_lds.  One
+// Staging: a 4-deep ring of 32 KiB LDS stages filled by global_load_lds.  One
 // load instruction moves 8 rows x 128 contiguous bytes (full lines: lane
 // 8r+s fetches 16-byte segment s^(r&7) of row r), so a 16-row block is two
 // loads and its LDS image is [row][segment ^ (row&7)] -- the XOR keeps the
-// fragment reads conflict-free (each ds_read_b128 lane group hits 16
-// distinct 16-byte slots).  The loads for chunk c+NST issue between the
-// MFMAs of chunk c's last segment and stay in flight across NST-2 barriers
-// (counted `s_waitcnt vmcnt`, raw s_barrier; guide sec.5 'Pipelining across
-// barriers').  Each wave issues exactly KNN_GLDS loads per chunk: its
-// m-tile (2), its 16 queries (2), and a 256-byte slice of the tile's norms
-// (waves 4..7 load a spare copy), so the waits are static.
+// fragment reads conflict-free.  Each wave stages its own m-tile (loads 0,1)
+// and its own 16 queries (loads 2,3) of every chunk.
 //
-// Main loop, 4 segments per chunk, each 8 MFMAs interleaved (sched_barrier
-// pinned) with the LDS reads of the next segment's fragments:
-//   S0 (p0, mt0-3) S1 (p0, mt4-7) S2 (p1, mt0-3) | lgkmcnt(0), wait chunk
-//   c+1, barrier | S3 (p1, mt4-7).  The staging loads of chunk c+NST
-//   (into the stage the barrier freed) ride in S3(c) and S0-S2(c+1).
+// The schedule is branch-free: chunk x's load 0 issues in segment S3 of
+// chunk x-4 (after the barrier that freed its stage) and loads 1..3 in
+// S0..S2 of chunk x-3, one per segment.  Chunks past the end re-load the last valid chunk
+// (clamped address) into their stage, so every chunk issues exactly 4 loads
+// per wave and "chunk c+1 landed" is always `s_waitcnt vmcnt(8)` (guide
+// sec.5 'Pipelining across barriers'; LDS-DMA stays in flight across
+// barriers).  A straight-line body keeps the accumulators in place: the
+// previous loop (one flat loop with a conditional epilogue and a last-chunk
+// branch) made the register allocator shuttle them with v_mov + s_nop after
+// every S1/S3 MFMA.
 //
-// Loads per chunk and wave: 4 (corpus rows 2, queries 2), plus one 256-byte
-// norm slice on a tile's first chunk for waves 0..3 -- so the number a wave
-// may leave in flight is known per chunk and waited for exactly.
+// Corpus norms: one 1 KiB slice per tile, loaded two tiles ahead at the
+// start of a tile (all 8 waves: waves 4..7 repeat waves 0..3's bytes) into a
+// ring [tile&7][g][32] (row 4k+g at [g][k]); the >= 8 loads that follow it
+// before that tile's epilogue make the vmcnt(8) waits cover it.
+//
+// Segments per chunk, 8 MFMAs each (an m-tile's two k-steps back to back:
+// measured 1.2% faster than splitting the dependent pair) with the LDS
+// reads of the next segment's fragments between them:
+//   S0 (p0, mt0-3) S1 (p0, mt4-7) S2 (p1, mt0-3) | lgkmcnt(0), vmcnt(8),
+//   barrier | S3 (p1, mt4-7) reading chunk c+1's first fragments.
 //
 // LDS (one array, guide 'second __shared__ object' trap):
 //   stage s at s*32K: C [mt][row 16][128 B] (16 KiB), Q [w][row 16][128 B]
-//   NST*32K:          corpus norms ring [tile&7][g][32] (row 4k+g at [g][k])
+//   4*32K:            corpus norms ring [tile&7][g][32]
 // ---------------------------------------------------------------------------
-#define KNN_GLDS 5
-// chunk c+1 landed when at most 4*min(2, ahead) of this wave's loads remain
-// (a chunk's 5th load, a norm slice, only makes the wait conservative)
-__device__ __forceinline__ void wait_stage4(int ahead)
-{
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
+#define KNN_NST 4
+__device__ unsigned long long knn_dbg_rounds[256];   // tuning harness only (EPI 3)
 
-// s_waitcnt vmcnt(N) for a wave-uniform N in 0..15 (the count is an
-// immediate; waits on the wave's own loads only)
-__device__ __forceinline__ void wait_vm(int N)
+// LDS-DMA issue as inline asm (guide: glds16_asm).  Written through
+// __builtin_amdgcn_global_load_lds, the loads make hipcc's waitcnt pass treat
+// every later LDS read as racing a pending FLAT access and emit lgkmcnt(0)
+// ahead of each segment's first MFMA; hidden from it, their completion is
+// counted by this kernel's own `s_waitcnt vmcnt(N)`.  M0 (the wave-uniform
+// LDS destination) is written and restored inside the statement.
+__device__ __forceinline__ void glds16(const void *src, unsigned lds_dst)
 {
-    switch (N) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    }
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+}
+// Buffer form: wave-uniform base in a 128-bit descriptor (raw, stride 0),
+// 32-bit per-lane byte offset (half the address payload of the global form).
+typedef int knn_v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ knn_v4i knn_rsrc(const void *base)
+{
+    const unsigned long long a = (unsigned long long)(uintptr_t)base;
+    knn_v4i r;
+    r.x = (int)(unsigned)a;
+    r.y = (int)((unsigned)(a >> 32) & 0xffffu);
+    r.z = -1;                 // num_records: no bounds check in practice
+    r.w = 0x00020000;
+    return r;
+}
+__device__ __forceinline__ void bglds16(knn_v4i rsrc, unsigned voff, unsigned lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+}
+__device__ __forceinline__ void glds4(const void *src, unsigned lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
 }
 
 // EPI = 0 / ABL != 0 exist only for the tuning harness (tools/probe/kbench):
 // EPI 0 skips the top-k insertion; ABL bit 0 drops the staging loads, bit 1
-// the chunk barrier.  libknn instantiates <.., 1, 0>.
-template <int KL, int KS, int NST, int EPI = 1, int ABL = 0>
+// the chunk barrier, bit 4 raises waves 4..7 to s_setprio 1, bit 5 issues
+// each m-tile's x/y k-steps apart (4 MFMAs between the dependent pair), bit 6
+// stages every workgroup's queries from query block 0 and bit 7 the corpus
+// from the split's first tile (L2-resident: locality experiments; wrong
+// results); bit 8 stages 4-byte pieces (same issue count, a quarter of the
+// LDS-DMA bytes), bits 9/10 drop the corpus / query loads.  libknn
+// instantiates <.., 1, 0>; bit 11 issues each segment's load before its
+// first MFMA pair instead of after the second; bit 12 stages with
+// global_load_lds instead of buffer_load ... lds.  EPI 3 counts insertion
+// rounds per tile position into knn_dbg_rounds.
+template <int KL, int KS, int EPI = 1, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const double *__restrict__ qblk, const double *__restrict__ qnorm, size_t q_base, int nq,
     const double *__restrict__ cblk, const double *__restrict__ cnorm, size_t c_base, int nc,
     int n, int n_pad, int ntiles, int nsplit, int nqb, const double *__restrict__ meta,
     double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T,
-    int nq_pad)
+    int nq_pad, unsigned long long *__restrict__ qthr)
 {
+    constexpr int NST = KNN_NST;
     __shared__ __attribute__((aligned(16))) char smem[NST * 32768 + 8192];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, j16 = lane & 15;
     // split-major order: the first resident wave of workgroups shares one
     // corpus split, so its tiles are read from L2 by every XCD's workgroups
-    // (an XCD-grouped (qb, split) order measured no better: FETCH unchanged)
     const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;
     const int t_lo = (int)((long)split * ntiles / nsplit);
     const int t_hi = (int)((long)(split + 1) * ntiles / nsplit);
@@ -283,15 +309,31 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const int myq = qrow0 + 16 * wave + j16;          // block-local query row
     const long gq = (long)q_base + myq;
     const double qn = qnorm[myq];
+    // consume qn here: its first real use (the epilogue) would otherwise get
+    // a vmcnt(0) from hipcc that drains the staging ring once per tile
+    asm volatile("" ::"v"(qn));
     const int nfc = n_pad / KNN_BK;
+    if constexpr ((ABL & 16) != 0) {
+        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    }
 
     double L[KL];
     int I[KL];
 #pragma unroll
     for (int e = 0; e < KL; e++) { L[e] = KNN_INF; I[e] = -1; }
+    // Shared per-query bound across splits and ring steps (qthr, bits of a
+    // non-negative double, atomicMin).  Any split's thr bounds the query's
+    // KS-th candidate over ALL rows (>= KS distinct candidates lie below
+    // it), so a split may start filtering at the smallest bound published so
+    // far.  Every value ever stored is a valid bound, so a stale read only
+    // costs filter strength; the returning atomic reads it at the memory
+    // side.  part_T still records the bound this split filtered with.
     double thr = KNN_INF;
+    if (qthr != nullptr && myq < nq)
+        thr = __longlong_as_double((long long)atomicMin(qthr + myq, 0x7ff0000000000000ull));
+    asm volatile("" ::"v"(thr));
 
-    const int total = (mode == KNN_MODE_SCAN) ? 0 : (t_hi - t_lo) * nfc;
+    const int total = (mode == KNN_MODE_SCAN || t_hi <= t_lo) ? 0 : (t_hi - t_lo) * nfc;
 
     dbl4 acc[8];
 #pragma unroll
@@ -299,55 +341,60 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
 
     LDS_AS char *lds = (LDS_AS char *)smem;
 
-    // ---- staging cursor -------------------------------------------------
-    // load i of a chunk: i = 0,1 -> rows 8i..8i+7 of the wave's m-tile,
-    // i = 2,3 -> of its 16 queries, i = 4 -> norm slice.  Lane 8r+s reads
-    // segment s^(r&7) of row r: per-lane offsets are fixed, the chunk moves
-    // a wave-uniform base.
+    // ---- staging cursor (wave-uniform; clamps at the last chunk) ---------
     const int lr = lane >> 3, ls = lane & 7;
     const int seg_off = 2 * (ls ^ lr);                       // doubles within the 128-B row
     const int lane_c = (16 * wave + lr) * n_pad + seg_off;   // corpus row 16w+lr of a tile
-    const double *const qbase = qblk + (size_t)(qrow0 + 16 * wave + lr) * n_pad + seg_off;
+    const int lane_q = (16 * wave + lr) * n_pad + seg_off;    // query row 16w+lr of the block
+    const double *const qbase = qblk + (size_t)((ABL & 64) ? 0 : qrow0) * n_pad + lane_q;
     // norms land permuted as [g][k] = norm of row 4k+g (4-byte pieces)
     const int cn_unit = (wave & 3) * 64 + lane;              // 4-byte unit 0..255
     const int cn_p = cn_unit >> 1;
     const int cn_src_off = ((cn_p & 31) * 4 + (cn_p >> 5)) * 8 + (cn_unit & 1) * 4;
-    int s_c = 0, s_t = t_lo, s_fc = 0;                       // next chunk to stage
+    int s_c = 0, s_t = t_lo, s_fc = 0;                       // chunk being staged
     auto glds1 = [&](int i) {
         if constexpr ((ABL & 1) != 0) return;
-        if constexpr ((ABL & 4) != 0) { if (i == 2 || i == 3) return; }   // no query loads
-        if constexpr ((ABL & 8) != 0) { if (i < 2) return; }              // no corpus loads
-        LDS_AS char *dst = lds + (s_c & (NST - 1)) * 32768 + wave * 2048;
+        const unsigned dst = (unsigned)(uintptr_t)(lds + (s_c & (NST - 1)) * 32768 + wave * 2048);
         const size_t fo = (size_t)KNN_BK * s_fc;
-        const double *csrc = cblk + (size_t)s_t * KNN_TC * n_pad + fo + lane_c;
+        const double *csrc = cblk + (size_t)((ABL & 128) ? t_lo : s_t) * KNN_TC * n_pad + fo + lane_c;
         const double *qsrc = qbase + fo;
-        if (i == 0) __builtin_amdgcn_global_load_lds((const void *)csrc, (LDS_AS void *)dst, 16, 0, 0);
-        if (i == 1) __builtin_amdgcn_global_load_lds((const void *)(csrc + 8 * (size_t)n_pad),
-                                                     (LDS_AS void *)(dst + 1024), 16, 0, 0);
-        if (i == 2) __builtin_amdgcn_global_load_lds((const void *)qsrc, (LDS_AS void *)(dst + 16384), 16, 0, 0);
-        if (i == 3) __builtin_amdgcn_global_load_lds((const void *)(qsrc + 8 * (size_t)n_pad),
-                                                     (LDS_AS void *)(dst + 17408), 16, 0, 0);
-        if (i == 4 && s_fc == 0 && wave < 4) {
-            LDS_AS char *ndst = lds + NST * 32768 + (s_t & 7) * 1024 + wave * 256;
-            __builtin_amdgcn_global_load_lds(
-                (const void *)((const char *)(cnorm + (size_t)s_t * KNN_TC) + cn_src_off),
-                (LDS_AS void *)ndst, 4, 0, 0);
+        if constexpr ((ABL & 4096) == 0) {  // buffer form (default; 0.7 ms faster than global_load_lds)
+            const double *cb = cblk + (size_t)s_t * KNN_TC * n_pad + fo;
+            const double *qb0 = qblk + (size_t)qrow0 * n_pad + fo;
+            const unsigned vc = (unsigned)lane_c * 8u, vq = (unsigned)lane_q * 8u;
+            const unsigned r8 = 64u * (unsigned)n_pad;
+            if (i == 0) bglds16(knn_rsrc(cb), vc, dst);
+            if (i == 1) bglds16(knn_rsrc(cb), vc + r8, dst + 1024);
+            if (i == 2) bglds16(knn_rsrc(qb0), vq, dst + 16384);
+            if (i == 3) bglds16(knn_rsrc(qb0), vq + r8, dst + 17408);
+        } else if constexpr ((ABL & 256) != 0) {   // 4-byte pieces: issue count kept, LDS writes / 4
+            if (i == 0 && (ABL & 512) == 0) glds4(csrc, dst);
+            if (i == 1 && (ABL & 512) == 0) glds4(csrc + 8 * (size_t)n_pad, dst + 1024);
+            if (i == 2 && (ABL & 1024) == 0) glds4(qsrc, dst + 16384);
+            if (i == 3 && (ABL & 1024) == 0) glds4(qsrc + 8 * (size_t)n_pad, dst + 17408);
+        } else {
+            if (i == 0 && (ABL & 512) == 0) glds16(csrc, dst);
+            if (i == 1 && (ABL & 512) == 0) glds16(csrc + 8 * (size_t)n_pad, dst + 1024);
+            if (i == 2 && (ABL & 1024) == 0) glds16(qsrc, dst + 16384);
+            if (i == 3 && (ABL & 1024) == 0) glds16(qsrc + 8 * (size_t)n_pad, dst + 17408);
         }
     };
     auto advance = [&]() {
         s_c++;
-        if (++s_fc == nfc) {
-            s_fc = 0;
-            s_t++;
+        if (s_c < total) {
+            if (++s_fc == nfc) {
+                s_fc = 0;
+                s_t++;
+            }
         }
     };
-    // staging loads this wave issues for chunk x whose feature chunk is fcx
-    // (0 if x is not staged); fcx comes from counters, never a division
-    auto nloads = [&](int x, int fcx) -> int {
-        if constexpr ((ABL & 1) != 0) return 0;
-        return x < total ? 4 + ((fcx == 0 && wave < 4) ? 1 : 0) : 0;
+    // norm slice of tile t (clamped to the split) into ring slot `slot`
+    auto gnorm = [&](int t, int slot) {
+        if constexpr ((ABL & 1) != 0) return;
+        const int ts = t < t_hi ? t : t_hi - 1;
+        const unsigned ndst = (unsigned)(uintptr_t)(lds + NST * 32768 + (slot & 7) * 1024 + (wave & 3) * 256);
+        glds4((const char *)(cnorm + (size_t)ts * KNN_TC) + cn_src_off, ndst);
     };
-    auto wrap = [&](int f) { return f >= nfc ? f - nfc : f; };   // f < 2*nfc
 
     // ---- epilogue of tile t: d^2, threshold filter, insertion ------------
     auto epilogue = [&](int t) {
@@ -408,6 +455,9 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 const int ii = (int)(c_base + row0 + 16 * (b >> 2) + g + 4 * (b & 3));
                 pend_all &= pend_all - 1;
                 list_insert<KL>(L, I, dd, ii);
+                if constexpr (EPI == 3) {
+                    if (threadIdx.x == 0) atomicAdd(&knn_dbg_rounds[(t - t_lo) < 255 ? t - t_lo : 255], 1ull);
+                }
             }
         }
 #pragma unroll
@@ -421,7 +471,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         lmin = fmin(lmin, __shfl_xor(lmin, 32));
         u = fmax(u, __shfl_xor(u, 16));
         u = fmax(u, __shfl_xor(u, 32));
-        thr = fmin(lmin, u);
+        thr = fmin(thr, fmin(lmin, u));   // monotone: rejections so far stay above it
     };
 
     // ---- fragments: quarter (p, h) = m-tiles 4h..4h+3 of piece p ---------
@@ -437,87 +487,84 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     auto rdq = [&](LDS_AS char *st, int p) {
         return *(const LDS_AS dbl2 *)(st + 16384 + wave * 2048 + (p ? fslot1 : fslot));
     };
-    auto mm = [&](const dbl2 (&f)[4], const dbl2 &b, int h, int j) {
-        acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].x, b.x, acc[4 * h + j], 0, 0, 0);
-        acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].y, b.y, acc[4 * h + j], 0, 0, 0);
-    };
-
-    // prologue: every stage is free, fill all NST of them
-    const int npre = total < NST ? total : NST;
-    for (int c = 0; c < npre; c++) {
-#pragma unroll
-        for (int i = 0; i < KNN_GLDS; i++) glds1(i);
-        advance();
-    }
-    // a chunk's staging loads are spread over S3 of one chunk and S0-S2 of
-    // the next (all after the barrier that freed its stage)
-    bool spread = false;
-    if (total > 0) {
-        wait_vm(nloads(1, 1 % nfc) + nloads(2, 2 % nfc) + nloads(3, 3 % nfc));   // chunk 0 landed
-        __builtin_amdgcn_s_barrier();
-        b0 = rdq(cs_of(0), 0);
-#pragma unroll
-        for (int j = 0; j < 4; j++) rd(cs_of(0), 0, 0, f0, j);
-    }
-    int fc_cur = 0;
-    for (int c = 0; c < total; c++) {
-        LDS_AS char *cs = cs_of(c);
-        // S0: (p0, mt0-3) on f0 || read (p0, mt4-7) into f1 [+ staging load 2]
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            rd(cs, 0, 1, f1, j);
-            if (j == 0 && spread) glds1(2);
-            mm(f0, b0, 0, j);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // S1: (p0, mt4-7) on f1 || read (p1, mt0-3) + B p1 [+ staging load 3]
-        b1 = rdq(cs, 1);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            rd(cs, 1, 0, f0, j);
-            if (j == 0 && spread) glds1(3);
-            mm(f1, b0, 1, j);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // S2: (p1, mt0-3) on f0 || read (p1, mt4-7) into f1 [+ staging load 4]
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            rd(cs, 1, 1, f1, j);
-            if (j == 0 && spread) glds1(4);
-            mm(f0, b1, 0, j);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (spread) {
-            advance();
-            spread = false;
-        }
-        if (c + 1 < total) {
-            if constexpr ((ABL & 2) == 0) {
-                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): f1/b1 landed (builtin:
-                // chunks c+2, c+3 may stay in flight: 4 loads each (+1 norm
-                // slice on a tile's first chunk, then this waits one early)
-                wait_stage4(total - 2 - c);           //  the waitcnt pass must see it)
-                __builtin_amdgcn_s_barrier();         // chunk c+1 visible; stage c%NST free
-            }
-            spread = s_c < total;                     // stage chunk s_c into stage c%NST
-            LDS_AS char *cs1 = cs_of(c + 1);
-            b0 = rdq(cs1, 0);
-            // S3: (p1, mt4-7) on f1 || read (p0, mt0-3) of c+1 [+ staging loads 0, 1]
+    // one segment: 8 MFMAs on quarter h with fragments f and query piece b;
+    // between them the reads `rdj(j)` of the next segment and one staging
+    // load `stage()` (sched_barrier-pinned order)
+    constexpr int SJ = (ABL & 2048) ? 0 : 2;   // m-tile pair after which a segment's load issues
+    auto segment = [&](const dbl2 (&f)[4], const dbl2 &b, int h, auto &&rdj, auto &&stage) {
+        if constexpr ((ABL & 32) == 0) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                rd(cs1, 0, 0, f0, j);
-                if (j < 2 && spread) glds1(j);
-                mm(f1, b1, 1, j);
+                rdj(j);
+                if (j == SJ) stage();
+                acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].x, b.x, acc[4 * h + j], 0, 0, 0);
+                acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].y, b.y, acc[4 * h + j], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < 4; j++) mm(f1, b1, 1, j);
+            for (int j = 0; j < 4; j++) {
+                acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].x, b.x, acc[4 * h + j], 0, 0, 0);
+                rdj(j);
+                if (j == SJ) stage();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].y, b.y, acc[4 * h + j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
-        if (++fc_cur == nfc) {
-            fc_cur = 0;
-            epilogue(t_lo + c / nfc);
+    };
+    auto nothing = [&]() {};
+
+    if (total > 0) {
+        // prologue: norms of the first two tiles, chunks 0..2 whole and
+        // chunk 3's load 0 (its loads 1..3 belong to S0..S2 of chunk 0)
+        gnorm(t_lo, t_lo);
+        gnorm(t_lo + 1, t_lo + 1);
+#pragma unroll
+        for (int x = 0; x < NST - 1; x++) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) glds1(i);
+            advance();
         }
+        glds1(0);
+        asm volatile("s_waitcnt vmcnt(9)" ::: "memory");    // norms + chunk 0 landed
+        __builtin_amdgcn_s_barrier();
+        b0 = rdq(cs_of(0), 0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) rd(cs_of(0), 0, 0, f0, j);
+
+        int c = 0;
+        for (int t = t_lo; t < t_hi; t++) {
+            gnorm(t + 2, t + 2);
+            for (int fc = 0; fc < nfc; fc++, c++) {
+                LDS_AS char *cs = cs_of(c);
+                // one staging load per segment, mid-segment: loads 1..3 of
+                // chunk c+3 in S0..S2, load 0 of chunk c+4 in S3 (after the
+                // barrier that freed its stage).  All 8 waves issuing right
+                // after the barrier cost 4% (measured); spread, ~1%.
+                // S0: (p0, mt0-3) on f0 || read (p0, mt4-7) into f1
+                segment(f0, b0, 0, [&](int j) { rd(cs, 0, 1, f1, j); }, [&]() { glds1(1); });
+                // S1: (p0, mt4-7) on f1 || read (p1, mt0-3) + B p1
+                b1 = rdq(cs, 1);
+                segment(f1, b0, 1, [&](int j) { rd(cs, 1, 0, f0, j); }, [&]() { glds1(2); });
+                // S2: (p1, mt0-3) on f0 || read (p1, mt4-7) into f1
+                segment(f0, b1, 0, [&](int j) { rd(cs, 1, 1, f1, j); }, [&]() { glds1(3); });
+                advance();
+                if constexpr ((ABL & 2) == 0) {
+                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this stage's reads done
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // chunk c+1 landed
+                    __builtin_amdgcn_s_barrier();         // chunk c+1 visible; stage c%4 free
+                }
+                LDS_AS char *cs1 = cs_of(c + 1);
+                b0 = rdq(cs1, 0);
+                // S3: (p1, mt4-7) on f1 || read (p0, mt0-3) of chunk c+1
+                segment(f1, b1, 1, [&](int j) { rd(cs1, 0, 0, f0, j); }, [&]() { glds1(0); });
+            }
+            epilogue(t);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // no LDS-DMA left in flight
     }
 
     if (myq < nq) {
@@ -527,7 +574,11 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             part_d[base + e] = L[e];
             part_i[base + e] = I[e];
         }
-        if (g == 0) part_T[(size_t)split * nq_pad + myq] = thr;
+        if (g == 0) {
+            part_T[(size_t)split * nq_pad + myq] = thr;
+            if (qthr != nullptr && thr < KNN_INF)
+                atomicMin(qthr + myq, (unsigned long long)__double_as_longlong(thr));
+        }
     }
 }
 
@@ -805,6 +856,20 @@ __global__ __launch_bounds__(256) void k_rescan_step(
     (void)q_base;
 }
 
+__global__ void k_fill_inf(double *p, int count)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) p[i] = KNN_INF;
+}
+
+extern "C" int knn_launch_fill_inf(double *p, int count, void *stream)
+{
+    if (count <= 0) return KNN_OK;
+    hipLaunchKernelGGL(k_fill_inf, dim3((unsigned)((count + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, p, count);
+    return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
+}
+
 __global__ void k_rescan_init(double *rs_d, int *rs_i, int count)
 {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -854,7 +919,7 @@ extern "C" int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_
                                     const double *cblk, size_t c_rows_pad, size_t c_base, int nc,
                                     int n, const double *meta, int nsplit,
                                     double *part_d, int *part_i, double *part_T, int nq_pad,
-                                    void *stream)
+                                    double *qthr, void *stream)
 {
     const int np = (int)knn_n_pad(n);
     const int nqb = (nq + KNN_TQ - 1) / KNN_TQ;
@@ -866,10 +931,11 @@ extern "C" int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_
         return KNN_ERR_INVALID;
     const double *qnorm = qblk + q_rows_pad * np;
     const double *cnorm = cblk + c_rows_pad * np;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, 4>),
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP>),
                        dim3((unsigned)(nqb * nsplit)), dim3(512), 0, (hipStream_t)stream,
                        qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles,
-                       nsplit, nqb, meta, part_d, part_i, part_T, nq_pad);
+                       nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
+                       (unsigned long long *)qthr);
     return hip_status();
 }
 

@@ -1,11 +1,12 @@
 // kbench: tuning harness for k_dist_topk (not part of libknn).
 //  1. sustained fp64 MFMA rate (long loop) and the clock it holds;
-//  2. k_dist_topk variants (main loop PIPE, epilogue on/off) on a 60000x784
+//  2. k_dist_topk variants (ABL/EPI ablations, see knn_kernels.hip) on a 60000x784
 //     integer corpus, timed with HIP events.
 #include "../../mpi-knn_amd/csrc/knn_kernels.hip"
 #include <cstdio>
 #include <vector>
 #include <cstdlib>
+#include <cstring>
 #define CK(x) do{hipError_t e_=(x); if(e_!=hipSuccess){printf("HIP %s @%d\n",hipGetErrorString(e_),__LINE__); exit(1);}}while(0)
 
 __global__ void mfma_sustain(double* out, long long* clk, int iters, double x)
@@ -34,19 +35,25 @@ __global__ void fill_int(double* X, size_t cnt, unsigned seed)
 }
 
 template <int EPI, int ABL = 0>
-float run(const double* blk, size_t rp, int m, int n, int nsplit, double* pd, int* pi, double* pT, int nq_pad, int reps)
+float run(const double* blk, size_t rp, int m, int n, int nsplit, double* pd, int* pi, double* pT, int nq_pad, int reps,
+          double* qthr = nullptr)
 {
     const int np = (int)knn_n_pad(n);
     const int nqb = (m + KNN_TQ - 1) / KNN_TQ, ntiles = (m + KNN_TC - 1) / KNN_TC;
     const double* norms = blk + rp * np;
     const double* meta = norms + rp;
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, 4, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
-                       blk, norms, (size_t)0, m, blk, norms, (size_t)0, m, n, np, ntiles, nsplit, nqb, meta, pd, pi, pT, nq_pad);
+    if (qthr) knn_launch_fill_inf(qthr, nq_pad, 0);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
+                       blk, norms, (size_t)0, m, blk, norms, (size_t)0, m, n, np, ntiles, nsplit, nqb, meta, pd, pi, pT, nq_pad,
+                           (unsigned long long*)qthr);
     CK(hipEventRecord(e0));
-    for (int r = 0; r < reps; r++)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, 4, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
-                           blk, norms, (size_t)0, m, blk, norms, (size_t)0, m, n, np, ntiles, nsplit, nqb, meta, pd, pi, pT, nq_pad);
+    for (int r = 0; r < reps; r++) {
+        if (qthr) knn_launch_fill_inf(qthr, nq_pad, 0);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
+                           blk, norms, (size_t)0, m, blk, norms, (size_t)0, m, n, np, ntiles, nsplit, nqb, meta, pd, pi, pT, nq_pad,
+                           (unsigned long long*)qthr);
+    }
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     return ms / reps;
@@ -77,15 +84,26 @@ int main(int argc, char** argv)
     CK(hipMalloc(&pd, (size_t)15 * nq_pad * 4 * KNN_KL * 8)); CK(hipMalloc(&pi, (size_t)15 * nq_pad * 4 * KNN_KL * 4));
     CK(hipMalloc(&pT, (size_t)15 * nq_pad * 8));
     const double flop = 2.0 * m * (double)m * n;
+    double* qthr; CK(hipMalloc(&qthr, (size_t)nq_pad * 8));
     for (int rep = 0; rep < 2; rep++) {
         const int s = 6;
         float p2 = run<1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
+        float pq = run<1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3, qthr);
         float p2n = run<0>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
         float a1 = run<0, 1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-        float a4 = run<0, 4>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-        float a8 = run<0, 8>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-        printf("full %.2f ms (%.1f TF) | noEPI %.2f  no-glds %.2f  no-query-glds %.2f  no-corpus-glds %.2f\n",
-               p2, flop / p2 / 1e9, p2n, a1, a4, a8);
+        printf("full %.2f ms (%.1f TF) | shared-bound %.2f ms (%.1f TF) | noEPI %.2f  no-glds %.2f\n",
+               p2, flop / p2 / 1e9, pq, flop / pq / 1e9, p2n, a1);
+    }
+    for (int v = 0; v < 2; v++) {
+        unsigned long long z[256] = {0};
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(knn_dbg_rounds), z, sizeof z));
+        run<3>(blk, rp, m, n, 6, pd, pi, pT, nq_pad, 1, v ? qthr : nullptr);   // 2 launches counted
+        CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(knn_dbg_rounds), sizeof z));
+        const int nqb = (m + KNN_TQ - 1) / KNN_TQ;
+        double tot = 0;
+        printf("%s: insertion rounds per wave by tile position:", v ? "shared-bound" : "own-bound");
+        for (int i = 0; i < 80; i++) { double r = z[i] / 2.0 / (nqb * 6.0); tot += r; if (i < 8 || i % 10 == 0) printf(" [%d]%.2f", i, r); }
+        printf("  total %.1f\n", tot);
     }
     return 0;
 }
