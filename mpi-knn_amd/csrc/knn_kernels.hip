@@ -198,28 +198,29 @@ __device__ __forceinline__ void wave_argmin(double &d, int &i)
 // feature 8p + 2g + e, so each lane's two k-steps of piece p are one 16-byte
 // slot (segment 4p+g of the row's 128 bytes): one ds_read_b128.
 //
-// Staging: a 4-deep ring of 32 KiB LDS stages filled by global_load_lds.  One
-// load instruction moves 8 rows x 128 contiguous bytes (full lines: lane
-// 8r+s fetches 16-byte segment s^(r&7) of row r), so a 16-row block is two
-// loads and its LDS image is [row][segment ^ (row&7)] -- the XOR keeps the
-// fragment reads conflict-free.  Each wave stages its own m-tile (loads 0,1)
-// and its own 16 queries (loads 2,3) of every chunk.
+// Staging: a 4-deep ring of 32 KiB LDS stages filled by LDS-DMA
+// (buffer_load_dwordx4 ... lds).  One load instruction moves 8 rows x 128
+// contiguous bytes (full lines: lane 8r+s fetches 16-byte segment s^(r&7) of
+// row r), so a 16-row block is two loads and its LDS image is
+// [row][segment ^ (row&7)] -- the XOR keeps the fragment reads conflict-free.
+// Each wave stages its own m-tile (loads 0,1) and its own 16 queries
+// (loads 2,3): 4 instructions per chunk, scalar addressing.
 //
 // The schedule is branch-free: chunk x's load 0 issues in segment S3 of
 // chunk x-4 (after the barrier that freed its stage) and loads 1..3 in
-// S0..S2 of chunk x-3, one per segment.  Chunks past the end re-load the last valid chunk
-// (clamped address) into their stage, so every chunk issues exactly 4 loads
-// per wave and "chunk c+1 landed" is always `s_waitcnt vmcnt(8)` (guide
-// sec.5 'Pipelining across barriers'; LDS-DMA stays in flight across
-// barriers).  A straight-line body keeps the accumulators in place: the
-// previous loop (one flat loop with a conditional epilogue and a last-chunk
-// branch) made the register allocator shuttle them with v_mov + s_nop after
-// every S1/S3 MFMA.
+// S0..S2 of chunk x-3, one per segment.  Chunks past the end re-load the
+// last valid chunk (clamped address) into their stage, so every chunk issues
+// the same loads and "chunk c+1 landed" is always one static
+// `s_waitcnt vmcnt(8)` (guide sec.5 'Pipelining across barriers'; LDS-DMA
+// stays in flight across barriers).  A straight-line body keeps the
+// accumulators in place: the previous loop (one flat loop with a conditional
+// epilogue and a last-chunk branch) made the register allocator shuttle them
+// with v_mov + s_nop after every S1/S3 MFMA.
 //
 // Corpus norms: one 1 KiB slice per tile, loaded two tiles ahead at the
-// start of a tile (all 8 waves: waves 4..7 repeat waves 0..3's bytes) into a
-// ring [tile&7][g][32] (row 4k+g at [g][k]); the >= 8 loads that follow it
-// before that tile's epilogue make the vmcnt(8) waits cover it.
+// start of a tile into a ring [tile&7][g][32] (row 4k+g at [g][k]; waves
+// 4..7 repeat the bytes of waves 0..3); the >= 8 loads that follow it before
+// that tile's epilogue make the vmcnt(8) waits cover it.
 //
 // Segments per chunk, 8 MFMAs each (an m-tile's two k-steps back to back:
 // measured 1.2% faster than splitting the dependent pair) with the LDS
@@ -240,13 +241,6 @@ __device__ unsigned long long knn_dbg_rounds[256];   // tuning harness only (EPI
 // ahead of each segment's first MFMA; hidden from it, their completion is
 // counted by this kernel's own `s_waitcnt vmcnt(N)`.  M0 (the wave-uniform
 // LDS destination) is written and restored inside the statement.
-__device__ __forceinline__ void glds16(const void *src, unsigned lds_dst)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
-}
 // Buffer form: wave-uniform base in a 128-bit descriptor (raw, stride 0),
 // 32-bit per-lane byte offset (half the address payload of the global form).
 typedef int knn_v4i __attribute__((ext_vector_type(4)));
@@ -267,6 +261,7 @@ __device__ __forceinline__ void bglds16(knn_v4i rsrc, unsigned voff, unsigned ld
                  "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
 }
+// 4-byte global form (corpus-norm slices: per-lane permuted gather)
 __device__ __forceinline__ void glds4(const void *src, unsigned lds_dst)
 {
     unsigned keep;
@@ -275,18 +270,14 @@ __device__ __forceinline__ void glds4(const void *src, unsigned lds_dst)
                  : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
 }
 
-// EPI = 0 / ABL != 0 exist only for the tuning harness (tools/probe/kbench):
-// EPI 0 skips the top-k insertion; ABL bit 0 drops the staging loads, bit 1
-// the chunk barrier, bit 4 raises waves 4..7 to s_setprio 1, bit 5 issues
-// each m-tile's x/y k-steps apart (4 MFMAs between the dependent pair), bit 6
-// stages every workgroup's queries from query block 0 and bit 7 the corpus
-// from the split's first tile (L2-resident: locality experiments; wrong
-// results); bit 8 stages 4-byte pieces (same issue count, a quarter of the
-// LDS-DMA bytes), bits 9/10 drop the corpus / query loads.  libknn
-// instantiates <.., 1, 0>; bit 11 issues each segment's load before its
-// first MFMA pair instead of after the second; bit 12 stages with
-// global_load_lds instead of buffer_load ... lds.  EPI 3 counts insertion
-// rounds per tile position into knn_dbg_rounds.
+// EPI != 1 / ABL != 0 exist only for the tuning harness (tools/probe/kbench):
+// EPI 0 skips the top-k insertion, EPI 3 counts insertion rounds per tile
+// position into knn_dbg_rounds.  ABL bits: 0 no staging loads, 1 no chunk
+// barrier, 4 s_setprio 1 on waves 4..7, 5 an m-tile's two k-steps 4 MFMAs
+// apart, 6 / 7 stage every workgroup's queries from block 0 / the corpus
+// from the split's first tile (L2-resident; wrong results), 11 each
+// segment's load before its first MFMA pair, 13 waves 0..3 stage for all
+// eight.  libknn instantiates <.., 1, 0>.
 template <int KL, int KS, int EPI = 1, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const double *__restrict__ qblk, const double *__restrict__ qnorm, size_t q_base, int nq,
@@ -344,39 +335,36 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // ---- staging cursor (wave-uniform; clamps at the last chunk) ---------
     const int lr = lane >> 3, ls = lane & 7;
     const int seg_off = 2 * (ls ^ lr);                       // doubles within the 128-B row
-    const int lane_c = (16 * wave + lr) * n_pad + seg_off;   // corpus row 16w+lr of a tile
-    const int lane_q = (16 * wave + lr) * n_pad + seg_off;    // query row 16w+lr of the block
-    const double *const qbase = qblk + (size_t)((ABL & 64) ? 0 : qrow0) * n_pad + lane_q;
     // norms land permuted as [g][k] = norm of row 4k+g (4-byte pieces)
     const int cn_unit = (wave & 3) * 64 + lane;              // 4-byte unit 0..255
     const int cn_p = cn_unit >> 1;
     const int cn_src_off = ((cn_p & 31) * 4 + (cn_p >> 5)) * 8 + (cn_unit & 1) * 4;
     int s_c = 0, s_t = t_lo, s_fc = 0;                       // chunk being staged
+    // Every wave stages its own m-tile and its own 16 queries.  All staging
+    // addresses are scalar (wave_s, not the VGPR wave index): deriving the
+    // LDS destination per load from a VGPR (v_readfirstlane into M0) cost
+    // 2.9 ms.  ABL bit 13 moves all staging to waves 0..3 (they load for
+    // their SIMD partner w+4 too): 0.6 ms slower once addressing is scalar.
+    const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+    constexpr bool SELF = (ABL & 8192) == 0;
+    const bool loader = SELF || wave_s < 4;
     auto glds1 = [&](int i) {
         if constexpr ((ABL & 1) != 0) return;
-        const unsigned dst = (unsigned)(uintptr_t)(lds + (s_c & (NST - 1)) * 32768 + wave * 2048);
+        if (!loader) return;
+        const unsigned r8 = 64u * (unsigned)n_pad;                 // 8 rows, bytes
         const size_t fo = (size_t)KNN_BK * s_fc;
-        const double *csrc = cblk + (size_t)((ABL & 128) ? t_lo : s_t) * KNN_TC * n_pad + fo + lane_c;
-        const double *qsrc = qbase + fo;
-        if constexpr ((ABL & 4096) == 0) {  // buffer form (default; 0.7 ms faster than global_load_lds)
-            const double *cb = cblk + (size_t)s_t * KNN_TC * n_pad + fo;
-            const double *qb0 = qblk + (size_t)qrow0 * n_pad + fo;
-            const unsigned vc = (unsigned)lane_c * 8u, vq = (unsigned)lane_q * 8u;
-            const unsigned r8 = 64u * (unsigned)n_pad;
-            if (i == 0) bglds16(knn_rsrc(cb), vc, dst);
-            if (i == 1) bglds16(knn_rsrc(cb), vc + r8, dst + 1024);
-            if (i == 2) bglds16(knn_rsrc(qb0), vq, dst + 16384);
-            if (i == 3) bglds16(knn_rsrc(qb0), vq + r8, dst + 17408);
-        } else if constexpr ((ABL & 256) != 0) {   // 4-byte pieces: issue count kept, LDS writes / 4
-            if (i == 0 && (ABL & 512) == 0) glds4(csrc, dst);
-            if (i == 1 && (ABL & 512) == 0) glds4(csrc + 8 * (size_t)n_pad, dst + 1024);
-            if (i == 2 && (ABL & 1024) == 0) glds4(qsrc, dst + 16384);
-            if (i == 3 && (ABL & 1024) == 0) glds4(qsrc + 8 * (size_t)n_pad, dst + 17408);
-        } else {
-            if (i == 0 && (ABL & 512) == 0) glds16(csrc, dst);
-            if (i == 1 && (ABL & 512) == 0) glds16(csrc + 8 * (size_t)n_pad, dst + 1024);
-            if (i == 2 && (ABL & 1024) == 0) glds16(qsrc, dst + 16384);
-            if (i == 3 && (ABL & 1024) == 0) glds16(qsrc + 8 * (size_t)n_pad, dst + 17408);
+        const double *cb = cblk + (size_t)((ABL & 128) ? t_lo : s_t) * KNN_TC * n_pad + fo;
+        const double *qb0 = qblk + (size_t)((ABL & 64) ? 0 : qrow0) * n_pad + fo;
+#pragma unroll
+        for (int hw = 0; hw < (SELF ? 1 : 2); hw++) {
+            const int ww = SELF ? wave_s : (wave_s & 3) + 4 * hw;
+            const unsigned dst = (unsigned)(uintptr_t)lds + (unsigned)(s_c & (NST - 1)) * 32768u +
+                                 (unsigned)ww * 2048u;
+            const unsigned vo = (unsigned)(((16 * ww + lr) * n_pad + seg_off) * 8);
+            if (i == 0) bglds16(knn_rsrc(cb), vo, dst);
+            if (i == 1) bglds16(knn_rsrc(cb), vo + r8, dst + 1024);
+            if (i == 2) bglds16(knn_rsrc(qb0), vo, dst + 16384);
+            if (i == 3) bglds16(knn_rsrc(qb0), vo + r8, dst + 17408);
         }
     };
     auto advance = [&]() {
@@ -391,6 +379,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // norm slice of tile t (clamped to the split) into ring slot `slot`
     auto gnorm = [&](int t, int slot) {
         if constexpr ((ABL & 1) != 0) return;
+        if (!loader) return;
         const int ts = t < t_hi ? t : t_hi - 1;
         const unsigned ndst = (unsigned)(uintptr_t)(lds + NST * 32768 + (slot & 7) * 1024 + (wave & 3) * 256);
         glds4((const char *)(cnorm + (size_t)ts * KNN_TC) + cn_src_off, ndst);
@@ -529,7 +518,10 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             advance();
         }
         glds1(0);
-        asm volatile("s_waitcnt vmcnt(9)" ::: "memory");    // norms + chunk 0 landed
+        // norms + chunk 0 landed: younger are chunks 1, 2 and chunk 3's
+        // load 0 -- 9 instructions per staged wave (18 for a loader of two)
+        if constexpr (SELF) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         b0 = rdq(cs_of(0), 0);
 #pragma unroll
@@ -554,7 +546,9 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 advance();
                 if constexpr ((ABL & 2) == 0) {
                     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this stage's reads done
-                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // chunk c+1 landed
+                    // chunk c+1 landed: chunks c+2, c+3 may stay in flight
+                    if constexpr (SELF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
                     __builtin_amdgcn_s_barrier();         // chunk c+1 visible; stage c%4 free
                 }
                 LDS_AS char *cs1 = cs_of(c + 1);

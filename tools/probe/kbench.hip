@@ -87,12 +87,20 @@ int main(int argc, char** argv)
     double* qthr; CK(hipMalloc(&qthr, (size_t)nq_pad * 8));
     for (int rep = 0; rep < 2; rep++) {
         const int s = 6;
-        float p2 = run<1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
+        const size_t pn = (size_t)s * nq_pad * 4 * KNN_KL;
+        std::vector<double> h1(pn), h2(pn);
+        run<1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 1);
+        CK(hipMemcpy(h1.data(), pd, pn * 8, hipMemcpyDeviceToHost));
+        run<1, 8192>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 1);
+        CK(hipMemcpy(h2.data(), pd, pn * 8, hipMemcpyDeviceToHost));
+        const bool ok1 = !memcmp(h1.data(), h2.data(), pn * 8);
         float pq = run<1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3, qthr);
-        float p2n = run<0>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-        float a1 = run<0, 1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3);
-        printf("full %.2f ms (%.1f TF) | shared-bound %.2f ms (%.1f TF) | noEPI %.2f  no-glds %.2f\n",
-               p2, flop / p2 / 1e9, pq, flop / pq / 1e9, p2n, a1);
+        float l1 = run<1, 8192>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3, qthr);
+        float p2n = run<0>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3, qthr);
+        float l1n = run<0, 8192>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3, qthr);
+        float a1 = run<0, 1>(blk, rp, m, n, s, pd, pi, pT, nq_pad, 3, qthr);
+        printf("full %.2f ms (%.1f TF) | loaders-0-3 %.2f ms (%.1f TF, lists %s) | noEPI %.2f  noEPI+loaders-0-3 %.2f  no-glds %.2f\n",
+               pq, flop / pq / 1e9, l1, flop / l1 / 1e9, ok1 ? "same" : "DIFF", p2n, l1n, a1);
     }
     for (int v = 0; v < 2; v++) {
         unsigned long long z[256] = {0};
