@@ -78,12 +78,29 @@ KNN_API int  knn_load_mat(const char *path, const char *xvar, const char *lvar,
 KNN_API void knn_free(void *p);
 
 /* ---------------------------------------------------------------------- *
+ * Element type of the search (dtype):
+ *   KNN_F64  the reference's arithmetic (results as described above).
+ *   KNN_F32  the points are rounded to fp32 and filtered with fp32 MFMA
+ *            (v_mfma_f32_16x16x4f32, 2x the fp64 rate).  Results are the
+ *            exact k nearest neighbours OF THE fp32-ROUNDED POINTS under the
+ *            reference's semantics: candidates are re-ranked by the
+ *            reference-order fp64 sum S over the rounded values, certified,
+ *            and rescanned when uncertified, exactly like the fp64 GEMM mode.
+ *            Integer data with n*max|x|^2 <= 2^23 and n*(max-min)^2 <= 2^24
+ *            (e.g. 8-bit pixels at n <= 128) is exact in fp32 arithmetic:
+ *            identical to KNN_F64.  Otherwise the only deviation from the
+ *            fp64 reference is the input rounding: |x - fp32(x)| <=
+ *            2^-24 |x| per coordinate, so each reported distance is within
+ *            2^-24 * (|q| + |c|) of the reference's (tests/test_gpu_f32.py).
+ * ---------------------------------------------------------------------- */
+
+/* ---------------------------------------------------------------------- *
  * One-call search on host arrays -- replaces the search section of
  * serial:54-93 and the whole ring of blk:81-244 / nb:91-259.
  * X: m x n fp64 in `layout`; labels (nullable, m doubles) fill .label;
  * ngpus >= 1 GPUs of this node (the corpus rotates over an RCCL ring when
- * ngpus > 1; results are byte-identical for every ngpus); dtype must be
- * KNN_F64 in this build.  out: caller-owned m*k records.
+ * ngpus > 1; results are byte-identical for every ngpus); dtype KNN_F64 or
+ * KNN_F32 (above).  out: caller-owned m*k records.
  * ---------------------------------------------------------------------- */
 KNN_API int knn_search(const double *X, size_t m, size_t n, int layout,
                const double *labels, int k, int ngpus, int dtype,
@@ -125,6 +142,11 @@ KNN_API size_t knn_block_bytes(size_t cap, size_t n);
  * all blocks of one search must be MAX-reduced into the d_meta passed to
  * knn_ctx_begin (a one-shot all-reduce of 8 doubles across ranks). */
 KNN_API size_t knn_block_meta_offset(size_t cap, size_t n);
+/* The same for blocks of element type dtype (KNN_F64 blocks above; KNN_F32
+ * blocks hold fp32 rows padded to 32 features and fp32 norms, then the
+ * same 8 fp64 meta words).  0 for an unknown dtype. */
+KNN_API size_t knn_block_bytes_dt(size_t cap, size_t n, int dtype);
+KNN_API size_t knn_block_meta_offset_dt(size_t cap, size_t n, int dtype);
 
 /* Pack rows (<= cap) points from a device source.  layout KNN_COLMAJOR:
  * element (i, j) at d_src[i + j*ld] (ld >= rows; the .mat layout,
@@ -132,6 +154,10 @@ KNN_API size_t knn_block_meta_offset(size_t cap, size_t n);
  * Computes norms and meta.  Replaces blk:100-109 / nb:110-119. */
 KNN_API int knn_block_pack(void *d_block, size_t cap, size_t rows, size_t n, const double *d_src,
                    size_t ld, int layout, void *stream);
+/* Pack into a block of element type dtype from a source of src_dtype
+ * (fp64 or fp32 device array, same layouts). */
+KNN_API int knn_block_pack_dt(void *d_block, int dtype, size_t cap, size_t rows, size_t n,
+                      const void *d_src, int src_dtype, size_t ld, int layout, void *stream);
 
 typedef struct knn_ctx knn_ctx_t;
 
@@ -139,6 +165,9 @@ typedef struct knn_ctx knn_ctx_t;
  * block_cap (knn_block_pack's cap) and hold at most block_cap rows. */
 KNN_API int knn_ctx_create(knn_ctx_t **ctx, int device, size_t nq, size_t n,
                    size_t block_cap, int k);
+/* A context over blocks of element type dtype (knn_ctx_create: KNN_F64). */
+KNN_API int knn_ctx_create_dt(knn_ctx_t **ctx, int device, size_t nq, size_t n,
+                      size_t block_cap, int k, int dtype);
 KNN_API int knn_ctx_destroy(knn_ctx_t *ctx);
 
 /* Start: the queries are the first nq rows of packed block d_qblock

@@ -30,6 +30,7 @@
 
 struct knn_ctx {
     int device;
+    int dtype;          /* element type of the packed blocks (KNN_F64 / KNN_F32) */
     size_t nq, nq_pad, n, block_cap;
     int k;
     int cus;
@@ -48,7 +49,7 @@ struct knn_ctx {
     int *rs_i;
     size_t rs_cap;
     /* current search */
-    const double *qblk;
+    const void *qblk;
     size_t q_base, q_rows_pad;
     const double *meta;
     int first_step;
@@ -84,26 +85,40 @@ void knn_free(void *p) { free(p); }
 
 double knn_last_search_seconds(void) { return g_last_search_s; }
 
-size_t knn_block_meta_offset(size_t cap, size_t n)
+static int dtype_ok(int dtype) { return dtype == KNN_F64 || dtype == KNN_F32; }
+
+size_t knn_block_meta_offset_dt(size_t cap, size_t n, int dtype)
 {
-    const size_t rp = knn_rows_pad(cap), np = knn_n_pad(n);
-    return (rp * np + rp) * sizeof(double);
+    if (!dtype_ok(dtype)) return 0;
+    const size_t rp = knn_rows_pad(cap), np = knn_n_pad_dt(n, dtype);
+    return (rp * np + rp) * knn_esize(dtype);
 }
 
-size_t knn_block_bytes(size_t cap, size_t n)
+size_t knn_block_bytes_dt(size_t cap, size_t n, int dtype)
 {
-    return knn_block_meta_offset(cap, n) + KNN_META_DOUBLES * sizeof(double);
+    if (!dtype_ok(dtype)) return 0;
+    return knn_block_meta_offset_dt(cap, n, dtype) + KNN_META_DOUBLES * sizeof(double);
+}
+
+size_t knn_block_meta_offset(size_t cap, size_t n) { return knn_block_meta_offset_dt(cap, n, KNN_F64); }
+
+size_t knn_block_bytes(size_t cap, size_t n) { return knn_block_bytes_dt(cap, n, KNN_F64); }
+
+int knn_block_pack_dt(void *d_block, int dtype, size_t cap, size_t rows, size_t n,
+                      const void *d_src, int src_dtype, size_t ld, int layout, void *stream)
+{
+    if (!d_block || !d_src || rows == 0 || n == 0 || rows > cap || cap > 0x7fffffffULL ||
+        n > 0x7fffffffULL || !dtype_ok(dtype) || !dtype_ok(src_dtype))
+        return KNN_ERR_INVALID;
+    if (layout == KNN_COLMAJOR ? ld < rows : (layout == KNN_ROWMAJOR ? ld < n : 1))
+        return KNN_ERR_INVALID;
+    return knn_launch_pack(d_block, dtype, cap, rows, n, d_src, src_dtype, ld, layout, stream);
 }
 
 int knn_block_pack(void *d_block, size_t cap, size_t rows, size_t n, const double *d_src,
                    size_t ld, int layout, void *stream)
 {
-    if (!d_block || !d_src || rows == 0 || n == 0 || rows > cap || cap > 0x7fffffffULL ||
-        n > 0x7fffffffULL)
-        return KNN_ERR_INVALID;
-    if (layout == KNN_COLMAJOR ? ld < rows : (layout == KNN_ROWMAJOR ? ld < n : 1))
-        return KNN_ERR_INVALID;
-    return knn_launch_pack((double *)d_block, cap, rows, n, d_src, ld, layout, stream);
+    return knn_block_pack_dt(d_block, KNN_F64, cap, rows, n, d_src, KNN_F64, ld, layout, stream);
 }
 
 static void ctx_free_buffers(knn_ctx_t *c)
@@ -163,10 +178,11 @@ static int prof_collect(knn_ctx_t *c)
     return KNN_OK;
 }
 
-int knn_ctx_create(knn_ctx_t **out, int device, size_t nq, size_t n, size_t block_cap, int k)
+int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t block_cap, int k,
+                      int dtype)
 {
     if (!out || nq == 0 || n == 0 || block_cap == 0 || k <= 0 || k > KNN_MAX_K ||
-        nq > 0x7fffffffULL || block_cap > 0x7fffffffULL)
+        nq > 0x7fffffffULL || block_cap > 0x7fffffffULL || !dtype_ok(dtype))
         return KNN_ERR_INVALID;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev)
@@ -179,6 +195,7 @@ int knn_ctx_create(knn_ctx_t **out, int device, size_t nq, size_t n, size_t bloc
     knn_ctx_t *c = (knn_ctx_t *)calloc(1, sizeof(*c));
     if (!c) return KNN_ERR_NOMEM;
     c->device = device;
+    c->dtype = dtype;
     c->nq = nq;
     c->nq_pad = knn_round_up(nq, KNN_TQ);
     c->n = n;
@@ -209,6 +226,11 @@ int knn_ctx_create(knn_ctx_t **out, int device, size_t nq, size_t n, size_t bloc
     return KNN_OK;
 }
 
+int knn_ctx_create(knn_ctx_t **out, int device, size_t nq, size_t n, size_t block_cap, int k)
+{
+    return knn_ctx_create_dt(out, device, nq, n, block_cap, k, KNN_F64);
+}
+
 int knn_ctx_destroy(knn_ctx_t *c)
 {
     if (!c) return KNN_OK;
@@ -231,7 +253,7 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
 {
     if (!c || !d_qblock || !d_meta || q_cap < c->nq) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
-    c->qblk = (const double *)d_qblock;
+    c->qblk = d_qblock;
     c->q_base = q_base;
     c->q_rows_pad = knn_rows_pad(q_cap);
     c->meta = d_meta;
@@ -274,17 +296,17 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     HIPCHK(hipSetDevice(c->device));
     const int nsplit = choose_splits(c, nc);
     c->nsplit_last = nsplit;
-    const double *cblk = (const double *)d_cblock;
+    const void *cblk = d_cblock;
     hipEvent_t *ev = NULL;
     if (c->prof_on && c->prof_pending < KNN_PROF_STEPS) {
         ev = &c->prof_ev[3 * c->prof_pending++];
         HIPCHK(hipEventRecord(ev[0], (hipStream_t)stream));
     }
-    RCHK(knn_launch_dist_topk(c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
+    RCHK(knn_launch_dist_topk(c->dtype, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
                               c->part_d, c->part_i, c->part_T, (int)c->nq_pad, c->qthr, stream));
     if (ev) HIPCHK(hipEventRecord(ev[1], (hipStream_t)stream));
-    RCHK(knn_launch_merge(c->part_d, c->part_i, c->part_T, nsplit, (int)c->nq, (int)c->nq_pad,
+    RCHK(knn_launch_merge(c->dtype, c->part_d, c->part_i, c->part_T, nsplit, (int)c->nq, (int)c->nq_pad,
                           c->first_step, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, cblk,
                           c_base, (int)nc, (int)c->n, c->meta, stream));
     if (ev) HIPCHK(hipEventRecord(ev[2], (hipStream_t)stream));
@@ -297,7 +319,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     if (!c || !d_out || c->first_step) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
-    RCHK(knn_launch_finalize(c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
+    RCHK(knn_launch_finalize(c->dtype, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
                              (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
                              c->fail_list, c->mode_dev, stream));
     int host[2];
@@ -332,9 +354,9 @@ int knn_ctx_rescan_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_
     if (!c || !d_cblock || nc == 0) return KNN_ERR_INVALID;
     if (c->nfail == 0) return KNN_OK;
     HIPCHK(hipSetDevice(c->device));
-    return knn_launch_rescan_step(c->fail_list, c->nfail, c->qblk, c->q_base,
-                                  (const double *)d_cblock, c_base, (int)nc, (int)c->n,
-                                  c->rs_d, c->rs_i, stream);
+    return knn_launch_rescan_step(c->dtype, c->fail_list, c->nfail, c->qblk, c->q_base,
+                                  d_cblock, c_base, (int)nc, (int)c->n, c->rs_d, c->rs_i,
+                                  stream);
 }
 
 int knn_ctx_rescan_end(knn_ctx_t *c, knn_neighbour_t *d_out, void *stream)
@@ -351,7 +373,7 @@ int knn_search_packed(knn_ctx_t *c, const void *d_block, size_t m, knn_neighbour
 {
     if (!c || !d_block || !d_out || m != c->nq || m != c->block_cap) return KNN_ERR_INVALID;
     const double *meta =
-        (const double *)((const char *)d_block + knn_block_meta_offset(m, c->n));
+        (const double *)((const char *)d_block + knn_block_meta_offset_dt(m, c->n, c->dtype));
     size_t unresolved = 0;
     RCHK(knn_ctx_begin(c, d_block, m, 0, meta, stream));
     RCHK(knn_ctx_step(c, d_block, m, 0, stream));
@@ -365,30 +387,31 @@ int knn_search_packed(knn_ctx_t *c, const void *d_block, size_t m, knn_neighbour
 
 /* Multi-GPU one-call path lives in knn_ring.c. */
 int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k, int ngpus,
-                         knn_neighbour_t *out, double *seconds);
+                         int dtype, knn_neighbour_t *out, double *seconds);
 
 int knn_search(const double *X, size_t m, size_t n, int layout, const double *labels, int k,
                int ngpus, int dtype, knn_neighbour_t *out)
 {
     if (!X || !out || m == 0 || n == 0 || k <= 0) return KNN_ERR_INVALID;
     if (k > KNN_MAX_K) return KNN_ERR_UNSUPPORTED;
-    if (dtype != KNN_F64) return KNN_ERR_UNSUPPORTED;
+    if (!dtype_ok(dtype)) return KNN_ERR_UNSUPPORTED;
     if (layout != KNN_COLMAJOR && layout != KNN_ROWMAJOR) return KNN_ERR_INVALID;
     if (ngpus < 1) return KNN_ERR_INVALID;
     int rc = KNN_OK;
     /* KNN_FORCE_RING=1 runs the RCCL ring driver even on one GPU (tests) */
     const char *force = getenv("KNN_FORCE_RING");
     if (ngpus > 1 || (force && force[0] == '1')) {
-        rc = knn_search_ring_host(X, m, n, layout, k, ngpus, out, &g_last_search_s);
+        rc = knn_search_ring_host(X, m, n, layout, k, ngpus, dtype, out, &g_last_search_s);
     } else {
         knn_ctx_t *ctx = NULL;
-        double *d_src = NULL, *d_blk = NULL;
+        double *d_src = NULL;
+        void *d_blk = NULL;
         knn_neighbour_t *d_out = NULL;
         hipEvent_t e0 = NULL, e1 = NULL;
-        rc = knn_ctx_create(&ctx, 0, m, n, m, k);
+        rc = knn_ctx_create_dt(&ctx, 0, m, n, m, k, dtype);
         if (rc) return rc;
         if (hipMalloc((void **)&d_src, m * n * sizeof(double)) != hipSuccess ||
-            hipMalloc((void **)&d_blk, knn_block_bytes(m, n)) != hipSuccess ||
+            hipMalloc(&d_blk, knn_block_bytes_dt(m, n, dtype)) != hipSuccess ||
             hipMalloc((void **)&d_out, m * (size_t)k * sizeof(knn_neighbour_t)) != hipSuccess) {
             rc = KNN_ERR_NOMEM;
             goto done1;
@@ -399,7 +422,8 @@ int knn_search(const double *X, size_t m, size_t n, int layout, const double *la
             goto done1;
         }
         hipEventRecord(e0, NULL);
-        rc = knn_block_pack(d_blk, m, m, n, d_src, layout == KNN_COLMAJOR ? m : n, layout, NULL);
+        rc = knn_block_pack_dt(d_blk, dtype, m, m, n, d_src, KNN_F64,
+                               layout == KNN_COLMAJOR ? m : n, layout, NULL);
         if (!rc) rc = knn_search_packed(ctx, d_blk, m, d_out, NULL);
         hipEventRecord(e1, NULL);
         if (!rc) {

@@ -15,7 +15,7 @@ extern "C" {
 /* Tile geometry shared by host and device. */
 #define KNN_TQ 128        /* queries per workgroup (8 waves x 16)      */
 #define KNN_TC 128        /* corpus rows per tile                      */
-#define KNN_BK 16         /* features per LDS chunk                    */
+#define KNN_BK 16         /* fp64 features per LDS chunk (128 B a row) */
 #define KNN_KL 16         /* per-lane candidate list capacity          */
 #define KNN_KP 32         /* per-query state / selection capacity      */
 #define KNN_ROW_ALIGN 128 /* packed-block row padding                  */
@@ -25,6 +25,8 @@ extern "C" {
 #define KNN_META_MAXNORM   1
 #define KNN_META_NONINT    2
 #define KNN_META_NONFINITE 3
+#define KNN_META_MAXPOS    4   /* max(x, 0)  */
+#define KNN_META_MAXNEG    5   /* max(-x, 0) */
 
 /* engine modes (decided on device from the reduced meta) */
 #define KNN_MODE_INT  0   /* integer data: GEMM-form d^2 is exact         */
@@ -34,28 +36,37 @@ extern "C" {
 static inline size_t knn_round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static inline size_t knn_rows_pad(size_t rows) { return knn_round_up(rows ? rows : 1, KNN_ROW_ALIGN); }
 static inline size_t knn_n_pad(size_t n) { return knn_round_up(n ? n : 1, KNN_BK); }
+/* element size and padded row length of a packed block of `dtype`
+ * (KNN_F64 / KNN_F32): rows are padded to whole 128-byte chunks */
+static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
+static inline size_t knn_n_pad_dt(size_t n, int dtype)
+{
+    return knn_round_up(n ? n : 1, 128 / knn_esize(dtype));
+}
 
-int knn_launch_pack(double *blk, size_t cap, size_t rows, size_t n, const double *src,
-                    size_t ld, int layout, void *stream);
-int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_t q_base, int nq,
-                         const double *cblk, size_t c_rows_pad, size_t c_base, int nc,
+/* Launchers.  dtype = element type of the packed blocks (KNN_F64 /
+ * KNN_F32); block pointers are untyped device pointers. */
+int knn_launch_pack(void *blk, int dtype, size_t cap, size_t rows, size_t n, const void *src,
+                    int src_dtype, size_t ld, int layout, void *stream);
+int knn_launch_dist_topk(int dtype, const void *qblk, size_t q_rows_pad, size_t q_base, int nq,
+                         const void *cblk, size_t c_rows_pad, size_t c_base, int nc,
                          int n, const double *meta, int nsplit,
                          double *part_d, int *part_i, double *part_T, int nq_pad,
                          double *qthr, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
-int knn_launch_merge(const double *part_d, const int *part_i, const double *part_T,
+int knn_launch_merge(int dtype, const double *part_d, const int *part_i, const double *part_T,
                      int nsplit, int nq, int nq_pad, int first_step,
                      double *st_d, double *st_x, int *st_i, double *st_T,
-                     const double *qblk, const double *cblk, size_t c_base, int nc,
+                     const void *qblk, const void *cblk, size_t c_base, int nc,
                      int n, const double *meta, void *stream);
-int knn_launch_finalize(const double *st_d, const double *st_x, const int *st_i,
-                        const double *st_T, const double *qblk, size_t q_rows_pad,
+int knn_launch_finalize(int dtype, const double *st_d, const double *st_x, const int *st_i,
+                        const double *st_T, const void *qblk, size_t q_rows_pad,
                         int nq, int n, int k, const double *meta,
                         knn_neighbour_t *out, int *fail_count, int *fail_list,
                         int *mode_out, void *stream);
 int knn_launch_rescan_init(double *rs_d, int *rs_i, int nfail, void *stream);
-int knn_launch_rescan_step(const int *fail_list, int nfail, const double *qblk,
-                           size_t q_base, const double *cblk, size_t c_base, int nc,
+int knn_launch_rescan_step(int dtype, const int *fail_list, int nfail, const void *qblk,
+                           size_t q_base, const void *cblk, size_t c_base, int nc,
                            int n, double *rs_d, int *rs_i, void *stream);
 int knn_launch_rescan_end(const int *fail_list, int nfail, const double *rs_d,
                           const int *rs_i, int k, knn_neighbour_t *out, void *stream);

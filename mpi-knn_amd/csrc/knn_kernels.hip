@@ -26,38 +26,85 @@
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef float flt4 __attribute__((ext_vector_type(4)));
 #define LDS_AS __attribute__((address_space(3)))
 
 static constexpr double KNN_INF = __builtin_inf();
 
 // ---------------------------------------------------------------------------
+// Element-type traits.  A staged chunk is 128 bytes of every row: 16 fp64
+// or 32 fp32 features.  One 16-byte LDS fragment holds KSF k-steps of the
+// 16x16x4 MFMA (2 fp64 / 4 fp32).  Result register r of lane group g holds
+// tile row ROW(g, r) (probed: tools/probe/mfma_probe, mfma_f32_probe).
+// ---------------------------------------------------------------------------
+template <typename T> struct KT;
+template <> struct KT<double> {
+    typedef dbl4 acc_t;
+    typedef dbl2 frag_t;
+    static constexpr int KSF = 2;
+    static constexpr double U = 1.1102230246251565e-16;   // 2^-53
+    __device__ static __forceinline__ acc_t mfma(double a, double b, acc_t c)
+    {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    __device__ static constexpr int row(int g, int r) { return g + 4 * r; }
+};
+template <> struct KT<float> {
+    typedef flt4 acc_t;
+    typedef flt4 frag_t;
+    static constexpr int KSF = 4;
+    static constexpr double U = 5.9604644775390625e-08;   // 2^-24
+    __device__ static __forceinline__ acc_t mfma(float a, float b, acc_t c)
+    {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    __device__ static constexpr int row(int g, int r) { return 4 * g + r; }
+};
+template <typename T> static constexpr int knn_bk() { return 128 / (int)sizeof(T); }
+
+// ---------------------------------------------------------------------------
 // Mode decision from the max-reduced meta (identical on every rank).
-//   INT : every value an integer and (2 max|x|)^2 n <= 2^51, so every
-//         partial sum of both the reference's sum of squares and of the
-//         GEMM form is an exact integer < 2^51, d^2 is bit-identical to the
-//         reference's S and sqrt is injective on it.
+//   INT : every value an integer and every partial sum of the GEMM form
+//         (norms, dot products, |q|^2+|c|^2, d^2) an integer below 2^p
+//         (p = 53 / 24), so d^2 is exact, bit-identical to the reference's
+//         S, and sqrt is injective on it.  fp64: (2 max|x|)^2 n
+//         <= 2^51; fp32: n max|x|^2 <= 2^23 and n (max - min)^2 <= 2^24.
 //   SCAN: non-finite values or norms near overflow -- no error bound.
 //   GEMM: everything else.
 // ---------------------------------------------------------------------------
+template <typename T>
 __device__ __forceinline__ int knn_mode(const double *meta, int n)
 {
-    if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e290))
-        return KNN_MODE_SCAN;
-    const double lim = 2251799813685248.0 / (4.0 * (double)n);   // 2^51 / 4n
-    double mx = meta[KNN_META_MAXABS];
-    if (meta[KNN_META_NONINT] == 0.0 && mx * mx <= lim) return KNN_MODE_INT;
-    return KNN_MODE_GEMM;
+    if constexpr (sizeof(T) == 8) {
+        if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e290))
+            return KNN_MODE_SCAN;
+        const double lim = 2251799813685248.0 / (4.0 * (double)n);   // 2^51 / 4n
+        double mx = meta[KNN_META_MAXABS];
+        if (meta[KNN_META_NONINT] == 0.0 && mx * mx <= lim) return KNN_MODE_INT;
+        return KNN_MODE_GEMM;
+    } else {
+        if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e37))
+            return KNN_MODE_SCAN;
+        const double mx = meta[KNN_META_MAXABS];
+        const double rg = meta[KNN_META_MAXPOS] + meta[KNN_META_MAXNEG];
+        if (meta[KNN_META_NONINT] == 0.0 && (double)n * mx * mx <= 8388608.0 &&
+            (double)n * rg * rg <= 16777216.0)
+            return KNN_MODE_INT;
+        return KNN_MODE_GEMM;
+    }
 }
 
 // Reference-order exact squared distance: S = S + (a-b)^2 over j = 0..n-1,
-// two roundings per feature, no FMA (knn-serial.c:76-85; pow(x,2) -> x*x).
-__device__ __attribute__((noinline)) double knn_exact_sq(const double *__restrict__ a,
-                                                         const double *__restrict__ b, int n)
+// two roundings per feature, no FMA (knn-serial.c:76-85; pow(x,2) -> x*x),
+// in fp64 on the block's values (fp32 blocks: the fp32-rounded inputs).
+template <typename T>
+__device__ __attribute__((noinline)) double knn_exact_sq(const T *__restrict__ a,
+                                                         const T *__restrict__ b, int n)
 {
 #pragma clang fp contract(off)
     double S = 0.0;
     for (int j = 0; j < n; j++) {
-        double t = a[j] - b[j];
+        double t = (double)a[j] - (double)b[j];
         double t2 = t * t;
         S = S + t2;
     }
@@ -65,15 +112,16 @@ __device__ __attribute__((noinline)) double knn_exact_sq(const double *__restric
 }
 
 // ---------------------------------------------------------------------------
-// k_pack: src (col-major, ld >= rows | row-major, ld >= n) -> padded row-major
-// block.  64x64 tiles through LDS so both sides stay coalesced.
+// k_pack: src (S = fp64 or fp32; col-major, ld >= rows | row-major, ld >= n)
+// -> padded row-major block of T.  64x64 tiles through LDS so both sides
+// stay coalesced.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pack(double *__restrict__ blk, size_t rows,
-                                              size_t rows_pad, int n, int n_pad,
-                                              const double *__restrict__ src, size_t ld,
-                                              int layout)
+template <typename T, typename S>
+__global__ __launch_bounds__(256) void k_pack(T *__restrict__ blk, size_t rows, size_t rows_pad,
+                                              int n, int n_pad, const S *__restrict__ src,
+                                              size_t ld, int layout)
 {
-    __shared__ double tile[64][65];
+    __shared__ T tile[64][65];
     const size_t i0 = (size_t)blockIdx.x * 64;
     const int j0 = blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -81,13 +129,13 @@ __global__ __launch_bounds__(256) void k_pack(double *__restrict__ blk, size_t r
         for (int jj = ty; jj < 64; jj += 4) {
             size_t i = i0 + tx;
             int j = j0 + jj;
-            tile[jj][tx] = (i < rows && j < n) ? src[i + (size_t)j * ld] : 0.0;
+            tile[jj][tx] = (i < rows && j < n) ? (T)src[i + (size_t)j * ld] : (T)0;
         }
     } else {
         for (int ii = ty; ii < 64; ii += 4) {
             size_t i = i0 + ii;
             int j = j0 + tx;
-            tile[tx][ii] = (i < rows && j < n) ? src[i * ld + j] : 0.0;
+            tile[tx][ii] = (i < rows && j < n) ? (T)src[i * ld + j] : (T)0;
         }
     }
     __syncthreads();
@@ -98,47 +146,50 @@ __global__ __launch_bounds__(256) void k_pack(double *__restrict__ blk, size_t r
     }
 }
 
-// One wave per row: squared norm + meta (max|x|, max norm, non-integer,
-// non-finite).  Block-reduced, then one atomicMax per block and word.
-__global__ __launch_bounds__(256) void k_norms(double *__restrict__ blk, size_t rows,
-                                               size_t rows_pad, int n, int n_pad)
+// One wave per row: squared norm (accumulated in fp64, stored as T) + meta
+// (max|x|, max norm, non-integer, non-finite, max(x)+, max(-x)+).
+// Block-reduced, then one atomicMax per block and word.
+template <typename T>
+__global__ __launch_bounds__(256) void k_norms(T *__restrict__ blk, size_t rows, size_t rows_pad,
+                                               int n, int n_pad)
 {
-    double *norms = blk + rows_pad * (size_t)n_pad;
-    double *meta = norms + rows_pad;
+    T *norms = blk + rows_pad * (size_t)n_pad;
+    double *meta = (double *)(norms + rows_pad);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    double mabs = 0.0, mnorm = 0.0, nonint = 0.0, nonfin = 0.0;
+    double mabs = 0.0, mnorm = 0.0, nonint = 0.0, nonfin = 0.0, mpos = 0.0, mneg = 0.0;
     for (size_t i = (size_t)blockIdx.x * 4 + wave; i < rows_pad; i += (size_t)gridDim.x * 4) {
-        const double *x = blk + i * n_pad;
+        const T *x = blk + i * n_pad;
         double s = 0.0;
         if (i < rows) {
             for (int j = lane; j < n; j += 64) {
-                double v = x[j];
+                double v = (double)x[j];
                 s = fma(v, v, s);
                 if (!__builtin_isfinite(v)) nonfin = 1.0;
                 else {
                     double a = fabs(v);
                     mabs = a > mabs ? a : mabs;
+                    mpos = v > mpos ? v : mpos;
+                    mneg = -v > mneg ? -v : mneg;
                     if (v != rint(v)) nonint = 1.0;
                 }
             }
         }
         for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-        if (lane == 0) norms[i] = s;
+        if (lane == 0) norms[i] = (T)s;
         if (s == s) mnorm = s > mnorm ? s : mnorm;
         else nonfin = 1.0;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        mabs = fmax(mabs, __shfl_xor(mabs, off));
-        mnorm = fmax(mnorm, __shfl_xor(mnorm, off));
-        nonint = fmax(nonint, __shfl_xor(nonint, off));
-        nonfin = fmax(nonfin, __shfl_xor(nonfin, off));
-    }
-    __shared__ double red[4][4];
+    double w[6] = {mabs, mnorm, nonint, nonfin, mpos, mneg};
+#pragma unroll
+    for (int q = 0; q < 6; q++)
+        for (int off = 32; off > 0; off >>= 1) w[q] = fmax(w[q], __shfl_xor(w[q], off));
+    __shared__ double red[4][6];
     if (lane == 0) {
-        red[wave][0] = mabs; red[wave][1] = mnorm; red[wave][2] = nonint; red[wave][3] = nonfin;
+#pragma unroll
+        for (int q = 0; q < 6; q++) red[wave][q] = w[q];
     }
     __syncthreads();
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < 6) {
         double v = fmax(fmax(red[0][threadIdx.x], red[1][threadIdx.x]),
                         fmax(red[2][threadIdx.x], red[3][threadIdx.x]));
         if (!(v >= 0.0)) v = __builtin_inf();  // NaN norm -> treat as overflow
@@ -154,14 +205,14 @@ __global__ __launch_bounds__(256) void k_norms(double *__restrict__ blk, size_t 
 // stable "lower index first" tie rule).  d >= L[KP-1] (incl. +inf,
 // NaN) is a no-op, so lanes without a candidate run it harmlessly.
 // ---------------------------------------------------------------------------
-template <int KP>
-__device__ __forceinline__ void list_insert(double (&L)[KP], int (&I)[KP], double d, int id)
+template <int KP, typename T>
+__device__ __forceinline__ void list_insert(T (&L)[KP], int (&I)[KP], T d, int id)
 {
     bool c_hi = d < L[KP - 1];
 #pragma unroll
     for (int e = KP - 1; e >= 0; e--) {
         bool c_lo = (e > 0) ? (d < L[e > 0 ? e - 1 : 0]) : false;
-        double t = c_lo ? L[e > 0 ? e - 1 : 0] : d;
+        T t = c_lo ? L[e > 0 ? e - 1 : 0] : d;
         int ti = c_lo ? I[e > 0 ? e - 1 : 0] : id;
         L[e] = c_hi ? t : L[e];
         I[e] = c_hi ? ti : I[e];
@@ -278,15 +329,20 @@ __device__ __forceinline__ void glds4(const void *src, unsigned lds_dst)
 // from the split's first tile (L2-resident; wrong results), 11 each
 // segment's load before its first MFMA pair, 13 waves 0..3 stage for all
 // eight.  libknn instantiates <.., 1, 0>.
-template <int KL, int KS, int EPI = 1, int ABL = 0>
+template <typename T, int KL, int KS, int EPI = 1, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void k_dist_topk(
-    const double *__restrict__ qblk, const double *__restrict__ qnorm, size_t q_base, int nq,
-    const double *__restrict__ cblk, const double *__restrict__ cnorm, size_t c_base, int nc,
+    const T *__restrict__ qblk, const T *__restrict__ qnorm, size_t q_base, int nq,
+    const T *__restrict__ cblk, const T *__restrict__ cnorm, size_t c_base, int nc,
     int n, int n_pad, int ntiles, int nsplit, int nqb, const double *__restrict__ meta,
     double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T,
     int nq_pad, unsigned long long *__restrict__ qthr)
 {
     constexpr int NST = KNN_NST;
+    constexpr int BK = knn_bk<T>();                   // features per 128-B chunk
+    constexpr int ES = (int)sizeof(T);
+    typedef typename KT<T>::acc_t acc_t;
+    typedef typename KT<T>::frag_t frag_t;
+    constexpr int KSF = KT<T>::KSF;
     __shared__ __attribute__((aligned(16))) char smem[NST * 32768 + 8192];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, j16 = lane & 15;
@@ -295,20 +351,20 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;
     const int t_lo = (int)((long)split * ntiles / nsplit);
     const int t_hi = (int)((long)(split + 1) * ntiles / nsplit);
-    const int mode = knn_mode(meta, n);
+    const int mode = knn_mode<T>(meta, n);
     const int qrow0 = qb * KNN_TQ;
     const int myq = qrow0 + 16 * wave + j16;          // block-local query row
     const long gq = (long)q_base + myq;
-    const double qn = qnorm[myq];
+    const T qn = qnorm[myq];
     // consume qn here: its first real use (the epilogue) would otherwise get
     // a vmcnt(0) from hipcc that drains the staging ring once per tile
     asm volatile("" ::"v"(qn));
-    const int nfc = n_pad / KNN_BK;
+    const int nfc = n_pad / BK;
     if constexpr ((ABL & 16) != 0) {
         if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     }
 
-    double L[KL];
+    T L[KL];
     int I[KL];
 #pragma unroll
     for (int e = 0; e < KL; e++) { L[e] = KNN_INF; I[e] = -1; }
@@ -319,26 +375,34 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // far.  Every value ever stored is a valid bound, so a stale read only
     // costs filter strength; the returning atomic reads it at the memory
     // side.  part_T still records the bound this split filtered with.
-    double thr = KNN_INF;
+    // (fp32: every published value came from an fp32 bound, so the
+    // conversion back is exact)
+    T thr = (T)KNN_INF;
     if (qthr != nullptr && myq < nq)
-        thr = __longlong_as_double((long long)atomicMin(qthr + myq, 0x7ff0000000000000ull));
+        thr = (T)__longlong_as_double((long long)atomicMin(qthr + myq, 0x7ff0000000000000ull));
     asm volatile("" ::"v"(thr));
 
     const int total = (mode == KNN_MODE_SCAN || t_hi <= t_lo) ? 0 : (t_hi - t_lo) * nfc;
 
-    dbl4 acc[8];
+    acc_t acc[8];
 #pragma unroll
-    for (int mt = 0; mt < 8; mt++) acc[mt] = (dbl4){0.0, 0.0, 0.0, 0.0};
+    for (int mt = 0; mt < 8; mt++) acc[mt] = (acc_t){0, 0, 0, 0};
 
     LDS_AS char *lds = (LDS_AS char *)smem;
 
     // ---- staging cursor (wave-uniform; clamps at the last chunk) ---------
     const int lr = lane >> 3, ls = lane & 7;
-    const int seg_off = 2 * (ls ^ lr);                       // doubles within the 128-B row
-    // norms land permuted as [g][k] = norm of row 4k+g (4-byte pieces)
-    const int cn_unit = (wave & 3) * 64 + lane;              // 4-byte unit 0..255
-    const int cn_p = cn_unit >> 1;
-    const int cn_src_off = ((cn_p & 31) * 4 + (cn_p >> 5)) * 8 + (cn_unit & 1) * 4;
+    const int seg_b = 16 * (ls ^ lr);                        // byte offset within the 128-B row
+    // norms land permuted as [g][k] = norm of tile row 16(k>>2) + ROW(g, k&3)
+    // (the rows lane group g holds, in register order), in 4-byte pieces:
+    // 256 pieces a tile for fp64 (waves 0..3), 128 for fp32 (waves 0,1);
+    // the other waves repeat the same bytes
+    constexpr int NU = 128 * ES / 4;                         // 4-byte pieces per tile
+    const int cn_unit = (__builtin_amdgcn_readfirstlane(wave) & (NU / 64 - 1)) * 64 + lane;
+    const int cn_p = ES == 8 ? cn_unit >> 1 : cn_unit;       // norm index g*32 + k
+    const int cn_k = cn_p & 31;
+    const int cn_src_off = (16 * (cn_k >> 2) + KT<T>::row(cn_p >> 5, cn_k & 3)) * ES +
+                           (ES == 8 ? (cn_unit & 1) * 4 : 0);
     int s_c = 0, s_t = t_lo, s_fc = 0;                       // chunk being staged
     // Every wave stages its own m-tile and its own 16 queries.  All staging
     // addresses are scalar (wave_s, not the VGPR wave index): deriving the
@@ -351,16 +415,16 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     auto glds1 = [&](int i) {
         if constexpr ((ABL & 1) != 0) return;
         if (!loader) return;
-        const unsigned r8 = 64u * (unsigned)n_pad;                 // 8 rows, bytes
-        const size_t fo = (size_t)KNN_BK * s_fc;
-        const double *cb = cblk + (size_t)((ABL & 128) ? t_lo : s_t) * KNN_TC * n_pad + fo;
-        const double *qb0 = qblk + (size_t)((ABL & 64) ? 0 : qrow0) * n_pad + fo;
+        const unsigned r8 = 8u * ES * (unsigned)n_pad;             // 8 rows, bytes
+        const size_t fo = (size_t)BK * s_fc;
+        const T *cb = cblk + (size_t)((ABL & 128) ? t_lo : s_t) * KNN_TC * n_pad + fo;
+        const T *qb0 = qblk + (size_t)((ABL & 64) ? 0 : qrow0) * n_pad + fo;
 #pragma unroll
         for (int hw = 0; hw < (SELF ? 1 : 2); hw++) {
             const int ww = SELF ? wave_s : (wave_s & 3) + 4 * hw;
             const unsigned dst = (unsigned)(uintptr_t)lds + (unsigned)(s_c & (NST - 1)) * 32768u +
                                  (unsigned)ww * 2048u;
-            const unsigned vo = (unsigned)(((16 * ww + lr) * n_pad + seg_off) * 8);
+            const unsigned vo = (unsigned)((16 * ww + lr) * n_pad * ES + seg_b);
             if (i == 0) bglds16(knn_rsrc(cb), vo, dst);
             if (i == 1) bglds16(knn_rsrc(cb), vo + r8, dst + 1024);
             if (i == 2) bglds16(knn_rsrc(qb0), vo, dst + 16384);
@@ -381,16 +445,17 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         if constexpr ((ABL & 1) != 0) return;
         if (!loader) return;
         const int ts = t < t_hi ? t : t_hi - 1;
-        const unsigned ndst = (unsigned)(uintptr_t)(lds + NST * 32768 + (slot & 7) * 1024 + (wave & 3) * 256);
+        const unsigned ndst = (unsigned)(uintptr_t)lds + NST * 32768u + (unsigned)(slot & 7) * 1024u +
+                              (unsigned)(wave_s & (NU / 64 - 1)) * 256u;
         glds4((const char *)(cnorm + (size_t)ts * KNN_TC) + cn_src_off, ndst);
     };
 
     // ---- epilogue of tile t: d^2, threshold filter, insertion ------------
     auto epilogue = [&](int t) {
-        const LDS_AS double *cng = (const LDS_AS double *)(lds + NST * 32768 + (t & 7) * 1024) + 32 * g;
-        const double lim = L[KL - 1] < thr ? L[KL - 1] : thr;
+        const LDS_AS T *cng = (const LDS_AS T *)(lds + NST * 32768 + (t & 7) * 1024) + 32 * g;
+        const T lim = L[KL - 1] < thr ? L[KL - 1] : thr;
         // INT mode: d^2 is exact and >= 0, so "S != 0" (serial:86) is d^2 > 0
-        const double zfloor = (mode == KNN_MODE_INT) ? 0.0 : -KNN_INF;
+        const T zfloor = (mode == KNN_MODE_INT) ? (T)0 : (T)-KNN_INF;
         // wave-uniform: only the block's last tile has rows >= nc, and only
         // tiles holding one of this wave's queries contain a self pair
         const int row0 = t * KNN_TC;
@@ -400,22 +465,28 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         unsigned pend_all = 0;
 #pragma unroll
         for (int mt = 0; mt < 8; mt++) {
-            const dbl2 n01 = ((const LDS_AS dbl2 *)cng)[2 * mt];
-            const dbl2 n23 = ((const LDS_AS dbl2 *)cng)[2 * mt + 1];
-            const double cnr[4] = {n01.x, n01.y, n23.x, n23.y};
+            T cnr[4];
+            if constexpr (ES == 8) {
+                const dbl2 n01 = ((const LDS_AS dbl2 *)cng)[2 * mt];
+                const dbl2 n23 = ((const LDS_AS dbl2 *)cng)[2 * mt + 1];
+                cnr[0] = n01.x; cnr[1] = n01.y; cnr[2] = n23.x; cnr[3] = n23.y;
+            } else {
+                const flt4 n4 = ((const LDS_AS flt4 *)cng)[mt];
+                cnr[0] = n4.x; cnr[1] = n4.y; cnr[2] = n4.z; cnr[3] = n4.w;
+            }
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                double v = fma(-2.0, acc[mt][r], qn + cnr[r]);
+                T v = fma((T)-2, acc[mt][r], qn + cnr[r]);
                 if (masked) {
-                    const int row = row0 + 16 * mt + g + 4 * r;
-                    v = (row < nc && (long)c_base + row != gq) ? v : KNN_INF;
+                    const int row = row0 + 16 * mt + KT<T>::row(g, r);
+                    v = (row < nc && (long)c_base + row != gq) ? v : (T)KNN_INF;
                 }
                 acc[mt][r] = v;
                 pend_all |= (v <= lim && v > zfloor) ? (1u << (4 * mt + r)) : 0u;
             }
         }
         if constexpr (EPI == 0) {
-            double s = acc[0][0];
+            T s = acc[0][0];
 #pragma unroll
             for (int mt = 0; mt < 8; mt++)
                 s = fmin(s, fmin(fmin(acc[mt][0], acc[mt][1]), fmin(acc[mt][2], acc[mt][3])));
@@ -430,18 +501,18 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             while (__ballot(pend_all != 0) != 0ull) {
                 const int b = pend_all ? __builtin_ctz(pend_all) : 0;
                 const bool b0 = b & 1, b1 = b & 2, b2 = b & 4, b3 = b & 8, b4 = b & 16;
-                double v[8];
+                T v[8];
 #pragma unroll
                 for (int mt = 0; mt < 8; mt++) {
-                    const double lo = b0 ? acc[mt][1] : acc[mt][0];
-                    const double hi = b0 ? acc[mt][3] : acc[mt][2];
+                    const T lo = b0 ? acc[mt][1] : acc[mt][0];
+                    const T hi = b0 ? acc[mt][3] : acc[mt][2];
                     v[mt] = b1 ? hi : lo;
                 }
-                const double w0 = b2 ? v[1] : v[0], w1 = b2 ? v[3] : v[2];
-                const double w2 = b2 ? v[5] : v[4], w3 = b2 ? v[7] : v[6];
-                const double x0 = b3 ? w1 : w0, x1 = b3 ? w3 : w2;
-                const double dd = pend_all ? (b4 ? x1 : x0) : KNN_INF;
-                const int ii = (int)(c_base + row0 + 16 * (b >> 2) + g + 4 * (b & 3));
+                const T w0 = b2 ? v[1] : v[0], w1 = b2 ? v[3] : v[2];
+                const T w2 = b2 ? v[5] : v[4], w3 = b2 ? v[7] : v[6];
+                const T x0 = b3 ? w1 : w0, x1 = b3 ? w3 : w2;
+                const T dd = pend_all ? (b4 ? x1 : x0) : (T)KNN_INF;
+                const int ii = (int)(c_base + row0 + 16 * (b >> 2) + KT<T>::row(g, b & 3));
                 pend_all &= pend_all - 1;
                 list_insert<KL>(L, I, dd, ii);
                 if constexpr (EPI == 3) {
@@ -450,12 +521,12 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             }
         }
 #pragma unroll
-        for (int mt = 0; mt < 8; mt++) acc[mt] = (dbl4){0.0, 0.0, 0.0, 0.0};
+        for (int mt = 0; mt < 8; mt++) acc[mt] = (acc_t){0, 0, 0, 0};
         if (!any) return;
         // shared threshold of the query's 4 lanes: their union holds
         // >= KS entries <= max_h L_h[KS/4-1], and every lane already
         // rejects >= min_h L_h[KL-1]
-        double lmin = L[KL - 1], u = L[KS / 4 - 1];
+        T lmin = L[KL - 1], u = L[KS / 4 - 1];
         lmin = fmin(lmin, __shfl_xor(lmin, 16));
         lmin = fmin(lmin, __shfl_xor(lmin, 32));
         u = fmax(u, __shfl_xor(u, 16));
@@ -468,39 +539,40 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // 16-byte slot of (row, segment 4p+g) in a 16-row image
     const int fslot = j16 * 128 + 16 * ((4 * 0 + g) ^ (j16 & 7));
     const int fslot1 = j16 * 128 + 16 * ((4 * 1 + g) ^ (j16 & 7));
-    dbl2 f0[4], f1[4];
-    dbl2 b0, b1;
-    auto rd = [&](LDS_AS char *st, int p, int h, dbl2 (&f)[4], int j) {
-        f[j] = *(const LDS_AS dbl2 *)(st + (4 * h + j) * 2048 + (p ? fslot1 : fslot));
+    frag_t f0[4], f1[4];
+    frag_t b0, b1;
+    auto rd = [&](LDS_AS char *st, int p, int h, frag_t (&f)[4], int j) {
+        f[j] = *(const LDS_AS frag_t *)(st + (4 * h + j) * 2048 + (p ? fslot1 : fslot));
     };
     auto rdq = [&](LDS_AS char *st, int p) {
-        return *(const LDS_AS dbl2 *)(st + 16384 + wave * 2048 + (p ? fslot1 : fslot));
+        return *(const LDS_AS frag_t *)(st + 16384 + wave * 2048 + (p ? fslot1 : fslot));
     };
     // one segment: 8 MFMAs on quarter h with fragments f and query piece b;
     // between them the reads `rdj(j)` of the next segment and one staging
     // load `stage()` (sched_barrier-pinned order)
     constexpr int SJ = (ABL & 2048) ? 0 : 2;   // m-tile pair after which a segment's load issues
-    auto segment = [&](const dbl2 (&f)[4], const dbl2 &b, int h, auto &&rdj, auto &&stage) {
+    auto segment = [&](const frag_t (&f)[4], const frag_t &b, int h, auto &&rdj, auto &&stage) {
         if constexpr ((ABL & 32) == 0) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 rdj(j);
                 if (j == SJ) stage();
-                acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].x, b.x, acc[4 * h + j], 0, 0, 0);
-                acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].y, b.y, acc[4 * h + j], 0, 0, 0);
+#pragma unroll
+                for (int e = 0; e < KSF; e++) acc[4 * h + j] = KT<T>::mfma(f[j][e], b[e], acc[4 * h + j]);
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].x, b.x, acc[4 * h + j], 0, 0, 0);
+                acc[4 * h + j] = KT<T>::mfma(f[j][0], b[0], acc[4 * h + j]);
                 rdj(j);
                 if (j == SJ) stage();
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                acc[4 * h + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[j].y, b.y, acc[4 * h + j], 0, 0, 0);
+            for (int e = 1; e < KSF; e++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[4 * h + j] = KT<T>::mfma(f[j][e], b[e], acc[4 * h + j]);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -565,13 +637,13 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         const size_t base = (((size_t)split * nq_pad + myq) * 4 + g) * KL;
 #pragma unroll
         for (int e = 0; e < KL; e++) {
-            part_d[base + e] = L[e];
+            part_d[base + e] = (double)L[e];
             part_i[base + e] = I[e];
         }
         if (g == 0) {
-            part_T[(size_t)split * nq_pad + myq] = thr;
-            if (qthr != nullptr && thr < KNN_INF)
-                atomicMin(qthr + myq, (unsigned long long)__double_as_longlong(thr));
+            part_T[(size_t)split * nq_pad + myq] = (double)thr;
+            if (qthr != nullptr && thr < (T)KNN_INF)
+                atomicMin(qthr + myq, (unsigned long long)__double_as_longlong((double)thr));
         }
     }
 }
@@ -584,19 +656,19 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
 // new in this step get their exact reference-order S from the resident
 // block (the only step at which their rows are on this device).
 // ---------------------------------------------------------------------------
-template <int KL, int KP>
+template <typename TE, int KL, int KP>
 __global__ __launch_bounds__(256) void k_merge(
     const double *__restrict__ part_d, const int *__restrict__ part_i,
     const double *__restrict__ part_T, int nsplit, int nq, int nq_pad, int first_step,
     double *__restrict__ st_d, double *__restrict__ st_x, int *__restrict__ st_i,
-    double *__restrict__ st_T, const double *__restrict__ qblk,
-    const double *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
+    double *__restrict__ st_T, const TE *__restrict__ qblk,
+    const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
     const double *__restrict__ meta)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + wave;
     if (q >= nq) return;
-    const int mode = knn_mode(meta, n);
+    const int mode = knn_mode<TE>(meta, n);
     const int nl = 4 * nsplit;
 
     const double *src_d = nullptr;
@@ -663,7 +735,7 @@ __global__ __launch_bounds__(256) void k_merge(
             sx = st_x[(size_t)q * KP + spos];
         } else {
             const int row = (int)((long)si - (long)c_base);
-            sx = knn_exact_sq(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n);
+            sx = knn_exact_sq<TE>(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n);
         }
     }
     // all reads of the old state are done (wave-private query) -> overwrite
@@ -685,17 +757,17 @@ __global__ __launch_bounds__(256) void k_merge(
 // them) nothing unseen can enter the list.  Uncertified queries go to the
 // rescan list.
 // ---------------------------------------------------------------------------
-template <int KP>
+template <typename TE, int KP>
 __global__ __launch_bounds__(256) void k_finalize(
     const double *__restrict__ st_d, const double *__restrict__ st_x,
     const int *__restrict__ st_i, const double *__restrict__ st_T,
-    const double *__restrict__ qnorm, int nq, int n, int k,
+    const TE *__restrict__ qnorm, int nq, int n, int k,
     const double *__restrict__ meta, knn_neighbour_t *__restrict__ out,
     int *__restrict__ fail_count, int *__restrict__ fail_list, int *__restrict__ mode_out)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + wave;
-    const int mode = knn_mode(meta, n);
+    const int mode = knn_mode<TE>(meta, n);
     if (blockIdx.x == 0 && threadIdx.x == 0) *mode_out = mode;
     if (q >= nq) return;
     knn_neighbour_t *o = out + (size_t)q * k;
@@ -750,8 +822,10 @@ __global__ __launch_bounds__(256) void k_finalize(
     if (nnz >= k) {
         const unsigned long long at = __ballot(valid && rank == k - 1);
         const double tau = __shfl(sx, __builtin_ctzll(at));
-        const double u = 1.1102230246251565e-16;  // 2^-53
-        const double E = 8.0 * (n + 4) * u * (qnorm[q] + meta[KNN_META_MAXNORM]);
+        // E bounds |GEMM-form d^2 - exact S| (unit roundoff of the filter
+        // arithmetic: 2^-53 fp64, 2^-24 fp32) plus the reference's own
+        const double u = KT<TE>::U;
+        const double E = 8.0 * (n + 4) * u * ((double)qnorm[q] + meta[KNN_META_MAXNORM]);
         ok = (Tb == KNN_INF) || ((Tb - E) > tau * (1.0 + 1.7763568394002505e-15));
     } else {
         ok = (Tb == KNN_INF);
@@ -782,10 +856,10 @@ __global__ __launch_bounds__(256) void k_finalize(
 // (distance = sqrt(S), S != 0), keeps a register list, then the 256 lists
 // and the running rescan list are merged by (distance, idx) in LDS.
 // ---------------------------------------------------------------------------
-template <int KP>
+template <typename TE, int KP>
 __global__ __launch_bounds__(256) void k_rescan_step(
-    const int *__restrict__ fail_list, const double *__restrict__ qblk, int n_pad_q,
-    size_t q_base, const double *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
+    const int *__restrict__ fail_list, const TE *__restrict__ qblk, int n_pad_q,
+    size_t q_base, const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
     double *__restrict__ rs_d, int *__restrict__ rs_i)
 {
     __shared__ double sh_d[256 + 1][KP];
@@ -795,13 +869,13 @@ __global__ __launch_bounds__(256) void k_rescan_step(
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int slot = blockIdx.x;
     const int q = fail_list[slot];
-    const double *qa = qblk + (size_t)q * n_pad_q;
+    const TE *qa = qblk + (size_t)q * n_pad_q;
     double L[KP];
     int I[KP];
 #pragma unroll
     for (int e = 0; e < KP; e++) { L[e] = KNN_INF; I[e] = 0x7fffffff; }
     for (int row = tid; row < nc; row += 256) {
-        const double S = knn_exact_sq(qa, cblk + (size_t)row * n_pad, n);
+        const double S = knn_exact_sq<TE>(qa, cblk + (size_t)row * n_pad, n);
         const double d = sqrt(S);
         if (d != 0.0) list_insert<KP>(L, I, d, (int)(c_base + row));
     }
@@ -893,29 +967,48 @@ __global__ void k_rescan_end(const int *__restrict__ fail_list, int nfail, int K
 // ---------------------------------------------------------------------------
 static int hip_status(void) { return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP; }
 
-extern "C" int knn_launch_pack(double *blk, size_t cap, size_t rows, size_t n,
-                               const double *src, size_t ld, int layout, void *stream)
+template <typename T, typename S>
+static int launch_pack(T *blk, size_t cap, size_t rows, size_t n, const S *src, size_t ld,
+                       int layout, hipStream_t s)
 {
-    hipStream_t s = (hipStream_t)stream;
-    const size_t rp = knn_rows_pad(cap), np = knn_n_pad(n);
-    double *meta = blk + rp * np + rp;
+    constexpr int dt = sizeof(T) == 8 ? KNN_F64 : KNN_F32;
+    const size_t rp = knn_rows_pad(cap), np = knn_n_pad_dt(n, dt);
+    double *meta = (double *)(blk + rp * np + rp);
     if (hipMemsetAsync(meta, 0, KNN_META_DOUBLES * sizeof(double), s) != hipSuccess)
         return KNN_ERR_HIP;
     dim3 grid((unsigned)((rp + 63) / 64), (unsigned)((np + 63) / 64));
-    hipLaunchKernelGGL(k_pack, grid, dim3(256), 0, s, blk, rows, rp, (int)n, (int)np, src, ld, layout);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack<T, S>), grid, dim3(256), 0, s, blk, rows, rp, (int)n,
+                       (int)np, src, ld, layout);
     unsigned nb = (unsigned)((rp / 4) < 4096 ? (rp / 4) : 4096);
     if (nb == 0) nb = 1;
-    hipLaunchKernelGGL(k_norms, dim3(nb), dim3(256), 0, s, blk, rows, rp, (int)n, (int)np);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_norms<T>), dim3(nb), dim3(256), 0, s, blk, rows, rp, (int)n,
+                       (int)np);
     return hip_status();
 }
 
-extern "C" int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_t q_base, int nq,
-                                    const double *cblk, size_t c_rows_pad, size_t c_base, int nc,
-                                    int n, const double *meta, int nsplit,
-                                    double *part_d, int *part_i, double *part_T, int nq_pad,
-                                    double *qthr, void *stream)
+extern "C" int knn_launch_pack(void *blk, int dtype, size_t cap, size_t rows, size_t n,
+                               const void *src, int src_dtype, size_t ld, int layout, void *stream)
 {
-    const int np = (int)knn_n_pad(n);
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == KNN_F64 && src_dtype == KNN_F64)
+        return launch_pack((double *)blk, cap, rows, n, (const double *)src, ld, layout, s);
+    if (dtype == KNN_F64 && src_dtype == KNN_F32)
+        return launch_pack((double *)blk, cap, rows, n, (const float *)src, ld, layout, s);
+    if (dtype == KNN_F32 && src_dtype == KNN_F64)
+        return launch_pack((float *)blk, cap, rows, n, (const double *)src, ld, layout, s);
+    if (dtype == KNN_F32 && src_dtype == KNN_F32)
+        return launch_pack((float *)blk, cap, rows, n, (const float *)src, ld, layout, s);
+    return KNN_ERR_INVALID;
+}
+
+template <typename T>
+static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int nq, const T *cblk,
+                            size_t c_rows_pad, size_t c_base, int nc, int n, const double *meta,
+                            int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
+                            double *qthr, hipStream_t s)
+{
+    constexpr int dt = sizeof(T) == 8 ? KNN_F64 : KNN_F32;
+    const int np = (int)knn_n_pad_dt(n, dt);
     const int nqb = (nq + KNN_TQ - 1) / KNN_TQ;
     const int ntiles = (nc + KNN_TC - 1) / KNN_TC;
     if (nqb <= 0 || nsplit <= 0) return KNN_ERR_INVALID;
@@ -923,41 +1016,77 @@ extern "C" int knn_launch_dist_topk(const double *qblk, size_t q_rows_pad, size_
     if ((size_t)nqb * KNN_TQ > q_rows_pad || (size_t)ntiles * KNN_TC > c_rows_pad ||
         nq_pad < nqb * KNN_TQ)
         return KNN_ERR_INVALID;
-    const double *qnorm = qblk + q_rows_pad * np;
-    const double *cnorm = cblk + c_rows_pad * np;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP>),
-                       dim3((unsigned)(nqb * nsplit)), dim3(512), 0, (hipStream_t)stream,
-                       qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles,
-                       nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
+    const T *qnorm = qblk + q_rows_pad * np;
+    const T *cnorm = cblk + c_rows_pad * np;
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KNN_KL, KNN_KP>), dim3((unsigned)(nqb * nsplit)),
+                       dim3(512), 0, s, qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np,
+                       ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
                        (unsigned long long *)qthr);
     return hip_status();
 }
 
-extern "C" int knn_launch_merge(const double *part_d, const int *part_i, const double *part_T,
-                                int nsplit, int nq, int nq_pad, int first_step,
-                                double *st_d, double *st_x, int *st_i, double *st_T,
-                                const double *qblk, const double *cblk, size_t c_base, int nc,
-                                int n, const double *meta, void *stream)
+extern "C" int knn_launch_dist_topk(int dtype, const void *qblk, size_t q_rows_pad, size_t q_base,
+                                    int nq, const void *cblk, size_t c_rows_pad, size_t c_base,
+                                    int nc, int n, const double *meta, int nsplit,
+                                    double *part_d, int *part_i, double *part_T, int nq_pad,
+                                    double *qthr, void *stream)
+{
+    if (dtype == KNN_F64)
+        return launch_dist_topk((const double *)qblk, q_rows_pad, q_base, nq, (const double *)cblk,
+                                c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i, part_T,
+                                nq_pad, qthr, (hipStream_t)stream);
+    if (dtype == KNN_F32)
+        return launch_dist_topk((const float *)qblk, q_rows_pad, q_base, nq, (const float *)cblk,
+                                c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i, part_T,
+                                nq_pad, qthr, (hipStream_t)stream);
+    return KNN_ERR_INVALID;
+}
+
+extern "C" int knn_launch_merge(int dtype, const double *part_d, const int *part_i,
+                                const double *part_T, int nsplit, int nq, int nq_pad,
+                                int first_step, double *st_d, double *st_x, int *st_i,
+                                double *st_T, const void *qblk, const void *cblk, size_t c_base,
+                                int nc, int n, const double *meta, void *stream)
 {
     if (4 * nsplit + 1 > 64) return KNN_ERR_INVALID;
-    const int np = (int)knn_n_pad(n);
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<KNN_KL, KNN_KP>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0,
-                       (hipStream_t)stream, part_d, part_i, part_T, nsplit, nq, nq_pad,
-                       first_step, st_d, st_x, st_i, st_T, qblk, cblk, c_base, nc, n, np, meta);
+    const int np = (int)knn_n_pad_dt(n, dtype);
+    const dim3 grid((unsigned)((nq + 3) / 4));
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == KNN_F64)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<double, KNN_KL, KNN_KP>), grid, dim3(256), 0, s,
+                           part_d, part_i, part_T, nsplit, nq, nq_pad, first_step, st_d, st_x,
+                           st_i, st_T, (const double *)qblk, (const double *)cblk, c_base, nc, n,
+                           np, meta);
+    else if (dtype == KNN_F32)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<float, KNN_KL, KNN_KP>), grid, dim3(256), 0, s,
+                           part_d, part_i, part_T, nsplit, nq, nq_pad, first_step, st_d, st_x,
+                           st_i, st_T, (const float *)qblk, (const float *)cblk, c_base, nc, n,
+                           np, meta);
+    else
+        return KNN_ERR_INVALID;
     return hip_status();
 }
 
-extern "C" int knn_launch_finalize(const double *st_d, const double *st_x, const int *st_i,
-                                   const double *st_T, const double *qblk, size_t q_rows_pad,
-                                   int nq, int n, int k, const double *meta,
+extern "C" int knn_launch_finalize(int dtype, const double *st_d, const double *st_x,
+                                   const int *st_i, const double *st_T, const void *qblk,
+                                   size_t q_rows_pad, int nq, int n, int k, const double *meta,
                                    knn_neighbour_t *out, int *fail_count, int *fail_list,
                                    int *mode_out, void *stream)
 {
     if (k <= 0 || k > KNN_KP) return KNN_ERR_INVALID;
-    const double *qnorm = qblk + q_rows_pad * knn_n_pad(n);
-    hipLaunchKernelGGL(k_finalize<KNN_KP>, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0,
-                       (hipStream_t)stream, st_d, st_x, st_i, st_T, qnorm, nq, n, k, meta,
-                       out, fail_count, fail_list, mode_out);
+    const size_t off = q_rows_pad * knn_n_pad_dt(n, dtype);
+    const dim3 grid((unsigned)((nq + 3) / 4));
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == KNN_F64)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_finalize<double, KNN_KP>), grid, dim3(256), 0, s, st_d,
+                           st_x, st_i, st_T, (const double *)qblk + off, nq, n, k, meta, out,
+                           fail_count, fail_list, mode_out);
+    else if (dtype == KNN_F32)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_finalize<float, KNN_KP>), grid, dim3(256), 0, s, st_d,
+                           st_x, st_i, st_T, (const float *)qblk + off, nq, n, k, meta, out,
+                           fail_count, fail_list, mode_out);
+    else
+        return KNN_ERR_INVALID;
     return hip_status();
 }
 
@@ -970,15 +1099,24 @@ extern "C" int knn_launch_rescan_init(double *rs_d, int *rs_i, int nfail, void *
     return hip_status();
 }
 
-extern "C" int knn_launch_rescan_step(const int *fail_list, int nfail, const double *qblk,
-                                      size_t q_base, const double *cblk, size_t c_base, int nc,
-                                      int n, double *rs_d, int *rs_i, void *stream)
+extern "C" int knn_launch_rescan_step(int dtype, const int *fail_list, int nfail,
+                                      const void *qblk, size_t q_base, const void *cblk,
+                                      size_t c_base, int nc, int n, double *rs_d, int *rs_i,
+                                      void *stream)
 {
     if (nfail <= 0) return KNN_OK;
-    const int np = (int)knn_n_pad(n);
-    hipLaunchKernelGGL(k_rescan_step<KNN_KP>, dim3((unsigned)nfail), dim3(256), 0,
-                       (hipStream_t)stream, fail_list, qblk, np, q_base, cblk, c_base, nc, n, np,
-                       rs_d, rs_i);
+    const int np = (int)knn_n_pad_dt(n, dtype);
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == KNN_F64)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_step<double, KNN_KP>), dim3((unsigned)nfail),
+                           dim3(256), 0, s, fail_list, (const double *)qblk, np, q_base,
+                           (const double *)cblk, c_base, nc, n, np, rs_d, rs_i);
+    else if (dtype == KNN_F32)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_step<float, KNN_KP>), dim3((unsigned)nfail),
+                           dim3(256), 0, s, fail_list, (const float *)qblk, np, q_base,
+                           (const float *)cblk, c_base, nc, n, np, rs_d, rs_i);
+    else
+        return KNN_ERR_INVALID;
     return hip_status();
 }
 

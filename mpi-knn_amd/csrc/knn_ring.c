@@ -109,7 +109,7 @@ static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int
 }
 
 int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k, int ngpus,
-                         knn_neighbour_t *out, double *seconds)
+                         int dtype, knn_neighbour_t *out, double *seconds)
 {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KNN_ERR_NODEVICE;
@@ -117,7 +117,8 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
     const int P = ngpus;
     const size_t R = (m + P - 1) / P;
     if (R == 0 || (size_t)(P - 1) * R >= m) return KNN_ERR_INVALID; /* every block non-empty */
-    const size_t bytes = knn_block_bytes(R, n);
+    const size_t bytes = knn_block_bytes_dt(R, n, dtype);
+    if (bytes == 0) return KNN_ERR_INVALID;
 
     ring_dev_t d[KNN_RING_MAX];
     memset(d, 0, sizeof(d));
@@ -158,7 +159,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             he = hipMemcpy(e->src, X + e->base * n, e->rows * n * sizeof(double),
                            hipMemcpyHostToDevice);
         if (he != hipSuccess) { rc = KNN_ERR_HIP; break; }
-        rc = knn_ctx_create(&e->ctx, g, e->rows, n, R, k);
+        rc = knn_ctx_create_dt(&e->ctx, g, e->rows, n, R, k, dtype);
     }
     for (int g = 0; g < P && !rc; g++)
         if (hipSetDevice(g) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = KNN_ERR_HIP;
@@ -171,9 +172,9 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         e->cur = e->qb;
         e->nxt = e->bufa;
         e->spare = e->bufb;
-        rc = knn_block_pack(e->qb, R, e->rows, n, e->src, layout == KNN_COLMAJOR ? e->rows : n,
-                            layout, e->cs);
-        if (!rc && hipMemcpyAsync(e->meta, (char *)e->qb + knn_block_meta_offset(R, n),
+        rc = knn_block_pack_dt(e->qb, dtype, R, e->rows, n, e->src, KNN_F64,
+                               layout == KNN_COLMAJOR ? e->rows : n, layout, e->cs);
+        if (!rc && hipMemcpyAsync(e->meta, (char *)e->qb + knn_block_meta_offset_dt(R, n, dtype),
                                   KNN_META_DOUBLES * sizeof(double), hipMemcpyDeviceToDevice,
                                   e->cs) != hipSuccess)
             rc = KNN_ERR_HIP;

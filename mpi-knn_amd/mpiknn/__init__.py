@@ -38,8 +38,10 @@ API_SYMBOLS = (
     "knn_classify", "knn_block_bytes", "knn_block_meta_offset", "knn_block_pack",
     "knn_ctx_create", "knn_ctx_destroy", "knn_ctx_begin", "knn_ctx_step", "knn_ctx_end",
     "knn_ctx_rescan_step", "knn_ctx_rescan_end", "knn_search_packed", "knn_ctx_info",
-    "knn_ctx_profile",
+    "knn_ctx_profile", "knn_block_bytes_dt", "knn_block_meta_offset_dt", "knn_block_pack_dt",
+    "knn_ctx_create_dt",
 )
+DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
 
 class KnnError(RuntimeError):
@@ -81,6 +83,10 @@ def _load():
         "knn_block_meta_offset": ([sz, sz], sz),
         "knn_block_pack": ([p, sz, sz, sz, p, sz, i, p], i),
         "knn_ctx_create": ([pp, i, sz, sz, sz, i], i),
+        "knn_block_bytes_dt": ([sz, sz, i], sz),
+        "knn_block_meta_offset_dt": ([sz, sz, i], sz),
+        "knn_block_pack_dt": ([p, i, sz, sz, sz, p, i, sz, i, p], i),
+        "knn_ctx_create_dt": ([pp, i, sz, sz, sz, i, i], i),
         "knn_ctx_destroy": ([p], i),
         "knn_ctx_begin": ([p, p, sz, sz, p, p], i),
         "knn_ctx_step": ([p, p, sz, sz, p], i),
@@ -142,11 +148,13 @@ def load_mat(path, xvar="train_X", lvar="train_labels"):
     return X, labels
 
 
-def search(X, k=30, ngpus=1, labels=None, layout="row"):
+def search(X, k=30, ngpus=1, labels=None, layout="row", dtype="f64"):
     """knn_search: all-kNN with the reference's serial semantics.
 
     X: (m, n) float64.  layout="row" passes C order, "col" Fortran order (the
-    .mat layout).  Returns (neighbours (m, k) NB_DTYPE, search seconds)."""
+    .mat layout).  dtype "f64" (reference arithmetic) or "f32" (fp32 MFMA
+    filter; exact kNN of the fp32-rounded points, include/knn.h).
+    Returns (neighbours (m, k) NB_DTYPE, search seconds)."""
     X = np.asarray(X, dtype=np.float64)
     m, n = X.shape
     if layout == "col":
@@ -155,7 +163,7 @@ def search(X, k=30, ngpus=1, labels=None, layout="row"):
         buf, lay = np.ascontiguousarray(X), ROWMAJOR
     out = np.zeros((m, k), dtype=NB_DTYPE)
     lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.float64)
-    rc = lib.knn_search(_ptr(buf), m, n, lay, _ptr(lab), k, ngpus, F64, _ptr(out))
+    rc = lib.knn_search(_ptr(buf), m, n, lay, _ptr(lab), k, ngpus, DTYPES[dtype], _ptr(out))
     _check(rc, "knn_search")
     return out, lib.knn_last_search_seconds()
 
@@ -174,18 +182,19 @@ def classify(nb, labels, nclasses=10, rule=VOTE_SERIAL):
 
 # ------------------------------------------------------ device-resident API
 
-def block_bytes(cap, n):
-    return lib.knn_block_bytes(cap, n)
+def block_bytes(cap, n, dtype="f64"):
+    return lib.knn_block_bytes_dt(cap, n, DTYPES[dtype])
 
 
-def block_meta_offset(cap, n):
-    return lib.knn_block_meta_offset(cap, n)
+def block_meta_offset(cap, n, dtype="f64"):
+    return lib.knn_block_meta_offset_dt(cap, n, DTYPES[dtype])
 
 
-def block_pack(d_block, cap, rows, n, d_src, ld, layout, stream=0):
-    """knn_block_pack on device pointers (ints).  layout COLMAJOR/ROWMAJOR."""
-    _check(lib.knn_block_pack(d_block, cap, rows, n, d_src, ld, layout, stream or None),
-           "knn_block_pack")
+def block_pack(d_block, cap, rows, n, d_src, ld, layout, stream=0, dtype="f64", src_dtype="f64"):
+    """knn_block_pack_dt on device pointers (ints).  layout COLMAJOR/ROWMAJOR;
+    dtype = block element type, src_dtype = that of d_src."""
+    _check(lib.knn_block_pack_dt(d_block, DTYPES[dtype], cap, rows, n, d_src, DTYPES[src_dtype],
+                                 ld, layout, stream or None), "knn_block_pack_dt")
 
 
 _live_contexts = weakref.WeakSet()
@@ -202,11 +211,11 @@ def _close_all():
 class Context:
     """knn_ctx_t: running neighbour lists of nq queries on one device."""
 
-    def __init__(self, device, nq, n, block_cap, k):
+    def __init__(self, device, nq, n, block_cap, k, dtype="f64"):
         self._h = ctypes.c_void_p()
-        _check(lib.knn_ctx_create(ctypes.byref(self._h), device, nq, n, block_cap, k),
-               "knn_ctx_create")
-        self.nq, self.n, self.block_cap, self.k = nq, n, block_cap, k
+        _check(lib.knn_ctx_create_dt(ctypes.byref(self._h), device, nq, n, block_cap, k,
+                                     DTYPES[dtype]), "knn_ctx_create_dt")
+        self.nq, self.n, self.block_cap, self.k, self.dtype = nq, n, block_cap, k, dtype
         _live_contexts.add(self)
 
     def close(self):

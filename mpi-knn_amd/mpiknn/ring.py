@@ -36,26 +36,26 @@ def partition(m, P):
 class GpuEngine:
     """libknn on one device; buffers are torch uint8 tensors on cuda."""
 
-    def __init__(self, torch, device, n, R, nq, k):
+    def __init__(self, torch, device, n, R, nq, k, dtype="f64"):
         import mpiknn
         self.torch, self.mk = torch, mpiknn
         self.dev = torch.device("cuda", device)
-        self.n, self.R, self.nq, self.k = n, R, nq, k
-        nb = mpiknn.block_bytes(R, n)
+        self.n, self.R, self.nq, self.k, self.dtype = n, R, nq, k, dtype
+        nb = mpiknn.block_bytes(R, n, dtype)
         self.qb = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
         self.bufa = torch.empty(nb, dtype=torch.uint8, device=self.dev)
         self.bufb = torch.empty(nb, dtype=torch.uint8, device=self.dev)
-        self.meta_off = mpiknn.block_meta_offset(R, n)
+        self.meta_off = mpiknn.block_meta_offset(R, n, dtype)
         self.meta = torch.zeros(mpiknn.META_DOUBLES, dtype=torch.float64, device=self.dev)
         self.out = torch.zeros(max(nq, 1) * k * 16, dtype=torch.uint8, device=self.dev)
-        self.ctx = mpiknn.Context(device, max(nq, 1), n, R, k)
+        self.ctx = mpiknn.Context(device, max(nq, 1), n, R, k, dtype)
 
     def stream(self):
         return self.torch.cuda.current_stream(self.dev).cuda_stream
 
     def pack(self, src, layout_col):
-        """src: this rank's rows on the device, (rows, n) float64 (any strides
-        matching the layout: col-major -> src.t() contiguous)."""
+        """src: this rank's rows on the device, (rows, n) float64 or float32
+        (any strides matching the layout: col-major -> src.t() contiguous)."""
         rows = src.shape[0]
         if layout_col:
             assert src.stride(0) == 1
@@ -65,8 +65,9 @@ class GpuEngine:
             assert src.stride(1) == 1
             ld = src.stride(0)
             lay = self.mk.ROWMAJOR
+        sdt = "f32" if src.dtype == self.torch.float32 else "f64"
         self.mk.block_pack(self.qb.data_ptr(), self.R, rows, self.n, src.data_ptr(), ld, lay,
-                           self.stream())
+                           self.stream(), dtype=self.dtype, src_dtype=sdt)
         self.meta.copy_(self.qb[self.meta_off:self.meta_off + 8 * self.mk.META_DOUBLES]
                         .view(self.torch.float64))
 

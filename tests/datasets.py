@@ -40,3 +40,22 @@ def mnist_like(m, n=784, seed=1234):
     X = protos[y] * scale + rng.normal(0, 40, (m, n))
     X = np.clip(np.rint(X), 0, 255)
     return X.astype(np.float64), (y + 1).astype(np.float64)
+
+
+def sift_like(m, n=128, clusters=1024, seed=0x51F7):
+    """BASELINE configs[3] shape (SIFT-like): Gaussian mixture of `clusters`
+    centres, clipped to [0, 255] and rounded -- integer-valued, fp32."""
+    rng = np.random.default_rng(seed)
+    centres = rng.uniform(0, 160, (clusters, n))
+    lab = rng.integers(0, clusters, m)
+    X = centres[lab] + rng.normal(0, 25, (m, n))
+    return np.clip(np.rint(X), 0, 255).astype(np.float64)
+
+
+def gist_like(m, n=960, clusters=256, seed=0x6157):
+    """BASELINE configs[4] shape (GIST-like): mixture in [0, 1), real-valued."""
+    rng = np.random.default_rng(seed)
+    centres = rng.uniform(0.1, 0.6, (clusters, n))
+    lab = rng.integers(0, clusters, m)
+    X = centres[lab] + rng.normal(0, 0.08, (m, n))
+    return np.clip(X, 0.0, np.nextafter(1.0, 0.0)).astype(np.float64)

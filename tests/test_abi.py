@@ -51,17 +51,25 @@ def test_invalid_arguments(knn):
     assert lib.knn_search(None, 4, 2, 1, None, 3, 1, 0, o) == knn.ERR_INVALID
     assert lib.knn_search(p, 4, 2, 7, None, 3, 1, 0, o) == knn.ERR_INVALID
     assert lib.knn_search(p, 4, 2, 1, None, 33, 1, 0, o) == knn.ERR_UNSUPPORTED
-    assert lib.knn_search(p, 4, 2, 1, None, 3, 1, 1, o) == knn.ERR_UNSUPPORTED
+    assert lib.knn_search(p, 4, 2, 1, None, 3, 1, 2, o) == knn.ERR_UNSUPPORTED  # no such dtype
     assert lib.knn_search(p, 4, 2, 1, None, 3, 0, 0, o) == knn.ERR_INVALID
     h = ctypes.c_void_p()
     assert lib.knn_ctx_create(ctypes.byref(h), 0, 0, 2, 4, 3) == knn.ERR_INVALID
     assert lib.knn_block_pack(None, 4, 4, 2, None, 4, 0, None) == knn.ERR_INVALID
+    assert lib.knn_ctx_create_dt(ctypes.byref(h), 0, 4, 2, 4, 3, 5) == knn.ERR_INVALID
+    assert lib.knn_block_pack_dt(None, 1, 4, 4, 2, None, 0, 4, 0, None) == knn.ERR_INVALID
+    assert lib.knn_block_pack_dt(p, 3, 4, 4, 2, p, 0, 4, 0, None) == knn.ERR_INVALID
 
 
 def test_block_layout(knn):
     # rows padded to 128, features to 16, + norms + 8 meta doubles
     assert knn.block_bytes(60000, 784) == (60032 * 784 + 60032 + 8) * 8
     assert knn.block_meta_offset(1, 1) == (128 * 16 + 128) * 8
+    # fp32 blocks: features padded to 32 (one 128-byte chunk), fp32 norms,
+    # then the same 8 fp64 meta words
+    assert knn.block_bytes(60000, 784, "f32") == (60032 * 800 + 60032) * 4 + 64
+    assert knn.block_meta_offset(1000, 128, "f32") == (1024 * 128 + 1024) * 4
+    assert knn.lib.knn_block_bytes_dt(10, 10, 7) == 0
 
 
 @pytest.mark.parametrize("rule", [0, 1, 2])

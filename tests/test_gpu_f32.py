@@ -1,0 +1,148 @@
+"""GPU parity of the fp32 path (dtype "f32", include/knn.h 'Element type').
+
+Contract: the fp32 path returns the EXACT k nearest neighbours of the
+fp32-rounded points under the reference's semantics (serial:72-93: sqrt of
+the j-ordered fp64 sum S, zeros excluded, ties by lower index).  So:
+  * against the oracle run on the rounded points: bit-exact, every mode;
+  * integer data (exactly representable): bit-exact to the fp64 reference,
+    both in fp32 INT mode (n max^2 <= 2^23) and fp32 GEMM mode (re-rank);
+  * against the oracle on the ORIGINAL points: every reported distance
+    within the stated bound 2^-24 (|q| + |c|) + 1e-12 d of the reference's
+    distance to that same neighbour.
+"""
+import numpy as np
+import pytest
+
+import datasets
+from test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def rounded(X):
+    return X.astype(np.float32).astype(np.float64)
+
+
+def run_engine(X, k, dtype="f32"):
+    """One-block search through the device API; returns (result, mode, unresolved)."""
+    import torch
+    import mpiknn.ring as ring
+    m, n = X.shape
+    dev = torch.device("cuda", 0)
+    e = ring.GpuEngine(torch, 0, n, m, m, k, dtype=dtype)
+    e.pack(torch.from_numpy(np.ascontiguousarray(X)).to(dev), layout_col=False)
+    e.begin(0)
+    e.step(e.qb, m, 0)
+    u = e.end()
+    if u:
+        e.step(e.qb, m, 0, rescan=True)
+        e.rescan_end()
+    mode, _ = e.ctx.info()
+    return e.result(), mode, u
+
+
+@pytest.mark.parametrize("m,n", [(3000, 128), (2000, 17)])
+def test_f32_integer_exact_mode(knn, oracle, m, n):
+    X = datasets.sift_like(m, n, clusters=64, seed=m + n)
+    ref = oracle.knn(X, 30)
+    got, mode, _ = run_engine(X, 30)
+    assert mode == 0, "expected fp32 integer-exact mode"
+    assert_same(got, ref, "sift_like f32 %dx%d" % (m, n))
+
+
+def test_f32_digits_matches_f64(knn, oracle):
+    X, y = datasets.digits()
+    ref = oracle.knn(X, 30, labels=y)
+    got, _ = knn.search(X, 30, labels=y, dtype="f32")
+    assert_same(got, ref, "digits f32")
+    assert knn.classify(got, y, 10, knn.VOTE_SERIAL)[1] == 1636
+
+
+def test_f32_mnist_gemm_mode_integer(knn, oracle):
+    # n = 784 pixels exceed the fp32 integer bound: fp32 GEMM filter + exact
+    # fp64 re-rank, still bit-exact (integers round to themselves)
+    X, _ = datasets.mnist_like(2500, 784, seed=21)
+    ref = oracle.knn(X, 30)
+    got, mode, u = run_engine(X, 30)
+    assert mode == 1
+    assert_same(got, ref, "mnist_like f32 gemm")
+    print("f32 gemm mnist: %d of %d queries rescanned" % (u, len(X)))
+
+
+@pytest.mark.parametrize("maker", ["digits_real", "gaussian", "gist_like"])
+def test_f32_real_valued(knn, oracle, maker):
+    if maker == "digits_real":
+        X = datasets.digits_real()[0]
+    elif maker == "gaussian":
+        X = np.random.default_rng(11).normal(0, 1, (1500, 96))
+    else:
+        X = datasets.gist_like(1200, 960, clusters=32)
+    Xr = rounded(X)
+    ref_r = oracle.knn(Xr, 30)
+    got, mode, u = run_engine(X, 30)
+    assert mode == 1
+    assert_same(got, ref_r, "%s f32 vs oracle on rounded points" % maker)
+    # distance tolerance against the reference on the original points
+    nrm = np.sqrt((X * X).sum(1))
+    for q in range(0, len(X), 97):
+        for slot in range(30):
+            j = got["idx"][q, slot] - 1
+            if j < 0:
+                continue
+            d_ref = np.sqrt(((X[q] - X[j]) ** 2).sum())
+            tol = 2.0 ** -24 * (nrm[q] + nrm[j]) + 1e-12 * d_ref
+            assert abs(got["distance"][q, slot] - d_ref) <= tol, (maker, q, slot)
+
+
+def test_f32_duplicates_and_ties(knn, oracle):
+    X, _ = datasets.digits()
+    X = np.vstack([X, X[:40], X[:40]]) / 3.0
+    ref = oracle.knn(rounded(X), 30)
+    got, _, _ = run_engine(X, 30)
+    assert_same(got, ref, "duplicates f32")
+    rng = np.random.default_rng(5)
+    B = rng.integers(0, 2, (1200, 12)).astype(np.float64)
+    assert_same(run_engine(B, 30)[0], oracle.knn(B, 30), "binary ties f32")
+
+
+def test_f32_nonfinite_scan(knn, oracle):
+    rng = np.random.default_rng(3)
+    X = rng.normal(0, 1, (300, 20))
+    X[5, 3] = np.nan
+    X[17, 0] = np.inf
+    got, mode, _ = run_engine(X, 30)
+    assert mode == 2
+    assert_same(got, oracle.knn(rounded(X), 30), "nan/inf f32")
+
+
+def test_f32_ring_blocks(knn, oracle):
+    """fp32 blocks rotated as in the ring (simulated on one GPU, P = 3)."""
+    import torch
+    import mpiknn.ring as ring
+    X = datasets.gist_like(1000, 300, clusters=16, seed=3)
+    m, n = X.shape
+    full = oracle.knn(rounded(X), 30)
+    dev = torch.device("cuda", 0)
+    Xd = torch.from_numpy(X).to(dev)
+    P = 3
+    R, blocks = ring.partition(m, P)
+    engines = []
+    for g in range(P):
+        base, rows = blocks[g]
+        e = ring.GpuEngine(torch, 0, n, R, rows, 30, dtype="f32")
+        e.pack(Xd[base:base + rows].float(), layout_col=False)   # fp32 source
+        engines.append(e)
+    meta = torch.stack([e.meta for e in engines]).max(dim=0).values
+    for g, e in enumerate(engines):
+        e.meta.copy_(meta)
+        base, rows = blocks[g]
+        e.begin(base)
+        for s in range(P):
+            b = (g - s) % P
+            e.step(engines[b].qb, blocks[b][1], blocks[b][0])
+        if e.end():
+            for s in range(P):
+                b = (g - s) % P
+                e.step(engines[b].qb, blocks[b][1], blocks[b][0], rescan=True)
+            e.rescan_end()
+        assert_same(e.result(), full[base:base + rows], "f32 ring rank %d" % g)

@@ -44,13 +44,13 @@ float run(const double* blk, size_t rp, int m, int n, int nsplit, double* pd, in
     const double* meta = norms + rp;
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     if (qthr) knn_launch_fill_inf(qthr, nq_pad, 0);
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<double, KNN_KL, KNN_KP, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
                        blk, norms, (size_t)0, m, blk, norms, (size_t)0, m, n, np, ntiles, nsplit, nqb, meta, pd, pi, pT, nq_pad,
                            (unsigned long long*)qthr);
     CK(hipEventRecord(e0));
     for (int r = 0; r < reps; r++) {
         if (qthr) knn_launch_fill_inf(qthr, nq_pad, 0);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<KNN_KL, KNN_KP, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<double, KNN_KL, KNN_KP, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
                            blk, norms, (size_t)0, m, blk, norms, (size_t)0, m, n, np, ntiles, nsplit, nqb, meta, pd, pi, pT, nq_pad,
                            (unsigned long long*)qthr);
     }
@@ -78,7 +78,7 @@ int main(int argc, char** argv)
     size_t rp = knn_rows_pad(m), np = knn_n_pad(n);
     double *src, *blk; CK(hipMalloc(&src, (size_t)m * n * 8)); CK(hipMalloc(&blk, (rp * np + rp + 8) * 8));
     fill_int<<<(unsigned)(((size_t)m * n + 255) / 256), 256>>>(src, (size_t)m * n, 1234u);
-    if (knn_launch_pack(blk, m, m, n, src, m, KNN_COLMAJOR, 0)) { printf("pack failed\n"); return 1; }
+    if (knn_launch_pack(blk, KNN_F64, m, m, n, src, KNN_F64, m, KNN_COLMAJOR, 0)) { printf("pack failed\n"); return 1; }
     int nq_pad = (int)knn_round_up(m, KNN_TQ);
     double *pd, *pT; int* pi;
     CK(hipMalloc(&pd, (size_t)15 * nq_pad * 4 * KNN_KL * 8)); CK(hipMalloc(&pi, (size_t)15 * nq_pad * 4 * KNN_KL * 4));
