@@ -60,8 +60,10 @@ enum knn_layout { KNN_COLMAJOR = 0, KNN_ROWMAJOR = 1 };
 enum knn_dtype  { KNN_F64 = 0, KNN_F32 = 1 };
 enum knn_vote   { KNN_VOTE_SERIAL = 0, KNN_VOTE_MPI = 1, KNN_VOTE_MAJORITY = 2 };
 
-/* Largest k served (the reference fixes NN = 30, serial:8 / blk:9). */
+/* Largest k served: KNN_F64 32 (the reference fixes NN = 30, serial:8 /
+ * blk:9); KNN_F32 128 (BASELINE configs[4]: k = 100). */
 #define KNN_MAX_K 32
+#define KNN_MAX_K_F32 128
 
 KNN_API const char *knn_strerror(int status);
 

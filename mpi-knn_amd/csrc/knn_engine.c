@@ -33,8 +33,11 @@ struct knn_ctx {
     int dtype;          /* element type of the packed blocks (KNN_F64 / KNN_F32) */
     size_t nq, nq_pad, n, block_cap;
     int k;
+    int kp, kl;         /* state capacity / per-lane list length serving k */
     int cus;
-    /* per-step partial lists of k_dist_topk, sized for KNN_MAX_SPLITS */
+    /* per-step partial lists of k_dist_topk, grown to the largest split
+     * count used so far (part_splits) */
+    int part_splits;
     double *part_d;
     int *part_i;
     double *part_T;
@@ -181,8 +184,9 @@ static int prof_collect(knn_ctx_t *c)
 int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t block_cap, int k,
                       int dtype)
 {
-    if (!out || nq == 0 || n == 0 || block_cap == 0 || k <= 0 || k > KNN_MAX_K ||
-        nq > 0x7fffffffULL || block_cap > 0x7fffffffULL || !dtype_ok(dtype))
+    if (!out || nq == 0 || n == 0 || block_cap == 0 || k <= 0 || !dtype_ok(dtype) ||
+        k > (dtype == KNN_F32 ? KNN_MAX_K_F32 : KNN_MAX_K) || nq > 0x7fffffffULL ||
+        block_cap > 0x7fffffffULL)
         return KNN_ERR_INVALID;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev)
@@ -201,18 +205,16 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     c->n = n;
     c->block_cap = block_cap;
     c->k = k;
+    c->kp = knn_kp_for(k);
+    c->kl = knn_kl_for(c->kp);
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
 
     const size_t np = c->nq_pad;
-    const size_t npart = (size_t)KNN_MAX_SPLITS * np * 4 * KNN_KL;
     int ok = 1;
-    ok &= hipMalloc((void **)&c->part_d, npart * sizeof(double)) == hipSuccess;
-    ok &= hipMalloc((void **)&c->part_i, npart * sizeof(int)) == hipSuccess;
-    ok &= hipMalloc((void **)&c->part_T, (size_t)KNN_MAX_SPLITS * np * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->qthr, np * sizeof(double)) == hipSuccess;
-    ok &= hipMalloc((void **)&c->st_d, np * KNN_KP * sizeof(double)) == hipSuccess;
-    ok &= hipMalloc((void **)&c->st_x, np * KNN_KP * sizeof(double)) == hipSuccess;
-    ok &= hipMalloc((void **)&c->st_i, np * KNN_KP * sizeof(int)) == hipSuccess;
+    ok &= hipMalloc((void **)&c->st_d, np * c->kp * sizeof(double)) == hipSuccess;
+    ok &= hipMalloc((void **)&c->st_x, np * c->kp * sizeof(double)) == hipSuccess;
+    ok &= hipMalloc((void **)&c->st_i, np * c->kp * sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->st_T, np * 2 * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->fail_count, sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->fail_list, np * sizeof(int)) == hipSuccess;
@@ -264,8 +266,18 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
     return KNN_OK;
 }
 
+/* bytes of partial lists per corpus split (k_dist_topk -> k_merge) */
+static size_t split_bytes(const knn_ctx_t *c)
+{
+    return c->nq_pad * (4 * (size_t)c->kl * (sizeof(double) + sizeof(int)) + sizeof(double));
+}
+
+#define KNN_PART_BUDGET ((size_t)2 << 30) /* partial-list bytes above one split */
+
 /* Corpus splits per query block: fill the CUs in whole waves of workgroups
- * (one 512-thread workgroup per CU), keep >= 4 tiles per split. */
+ * (one 512-thread workgroup per CU), keep >= 4 tiles per split, and take
+ * the fewest splits within 0.5% of the best fill (each split costs a
+ * partial-list pass and its memory, capped at KNN_PART_BUDGET). */
 static int choose_splits(const knn_ctx_t *c, size_t nc)
 {
     const char *env = getenv("KNN_SPLITS");
@@ -275,19 +287,41 @@ static int choose_splits(const knn_ctx_t *c, size_t nc)
         int s = atoi(env);
         return s > KNN_MAX_SPLITS ? KNN_MAX_SPLITS : s;
     }
-    int best = 1;
+    int smax = KNN_MAX_SPLITS;
+    const size_t per = split_bytes(c);
+    if (per > 0 && KNN_PART_BUDGET / per < (size_t)smax)
+        smax = KNN_PART_BUDGET / per > 1 ? (int)(KNN_PART_BUDGET / per) : 1;
+    double eff[KNN_MAX_SPLITS + 1] = {0};
     double best_eff = 0.0;
-    for (int s = 1; s <= KNN_MAX_SPLITS; s++) {
+    for (int s = 1; s <= smax; s++) {
         if (s > 1 && ntiles / s < 4) break;
         const long w = nqb * s;
         const long rounds = (w + c->cus - 1) / c->cus;
-        const double eff = (double)w / (double)(rounds * c->cus);
-        if (eff > best_eff + 1e-3) {
-            best_eff = eff;
-            best = s;
-        }
+        eff[s] = (double)w / (double)(rounds * c->cus);
+        if (eff[s] > best_eff) best_eff = eff[s];
     }
-    return best;
+    for (int s = 1; s <= smax; s++)
+        if (eff[s] >= best_eff - 5e-3) return s;
+    return 1;
+}
+
+static int ensure_part_buffers(knn_ctx_t *c, int nsplit)
+{
+    if (nsplit <= c->part_splits) return KNN_OK;
+    hipFree(c->part_d);
+    hipFree(c->part_i);
+    hipFree(c->part_T);
+    c->part_d = NULL;
+    c->part_i = NULL;
+    c->part_T = NULL;
+    c->part_splits = 0;
+    const size_t npart = (size_t)nsplit * c->nq_pad * 4 * (size_t)c->kl;
+    if (hipMalloc((void **)&c->part_d, npart * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&c->part_i, npart * sizeof(int)) != hipSuccess ||
+        hipMalloc((void **)&c->part_T, (size_t)nsplit * c->nq_pad * sizeof(double)) != hipSuccess)
+        return KNN_ERR_NOMEM;
+    c->part_splits = nsplit;
+    return KNN_OK;
 }
 
 int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, void *stream)
@@ -296,17 +330,18 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     HIPCHK(hipSetDevice(c->device));
     const int nsplit = choose_splits(c, nc);
     c->nsplit_last = nsplit;
+    RCHK(ensure_part_buffers(c, nsplit));
     const void *cblk = d_cblock;
     hipEvent_t *ev = NULL;
     if (c->prof_on && c->prof_pending < KNN_PROF_STEPS) {
         ev = &c->prof_ev[3 * c->prof_pending++];
         HIPCHK(hipEventRecord(ev[0], (hipStream_t)stream));
     }
-    RCHK(knn_launch_dist_topk(c->dtype, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
+    RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
                               c->part_d, c->part_i, c->part_T, (int)c->nq_pad, c->qthr, stream));
     if (ev) HIPCHK(hipEventRecord(ev[1], (hipStream_t)stream));
-    RCHK(knn_launch_merge(c->dtype, c->part_d, c->part_i, c->part_T, nsplit, (int)c->nq, (int)c->nq_pad,
+    RCHK(knn_launch_merge(c->dtype, c->kp, c->part_d, c->part_i, c->part_T, nsplit, (int)c->nq, (int)c->nq_pad,
                           c->first_step, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, cblk,
                           c_base, (int)nc, (int)c->n, c->meta, stream));
     if (ev) HIPCHK(hipEventRecord(ev[2], (hipStream_t)stream));
@@ -319,7 +354,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     if (!c || !d_out || c->first_step) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
-    RCHK(knn_launch_finalize(c->dtype, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
+    RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
                              (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
                              c->fail_list, c->mode_dev, stream));
     int host[2];
@@ -338,12 +373,12 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
             c->rs_i = NULL;
             c->rs_cap = 0;
             size_t cap = (size_t)c->nfail;
-            if (hipMalloc((void **)&c->rs_d, cap * KNN_KP * sizeof(double)) != hipSuccess ||
-                hipMalloc((void **)&c->rs_i, cap * KNN_KP * sizeof(int)) != hipSuccess)
+            if (hipMalloc((void **)&c->rs_d, cap * c->kp * sizeof(double)) != hipSuccess ||
+                hipMalloc((void **)&c->rs_i, cap * c->kp * sizeof(int)) != hipSuccess)
                 return KNN_ERR_NOMEM;
             c->rs_cap = cap;
         }
-        RCHK(knn_launch_rescan_init(c->rs_d, c->rs_i, c->nfail, stream));
+        RCHK(knn_launch_rescan_init(c->kp, c->rs_d, c->rs_i, c->nfail, stream));
     }
     return KNN_OK;
 }
@@ -354,7 +389,7 @@ int knn_ctx_rescan_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_
     if (!c || !d_cblock || nc == 0) return KNN_ERR_INVALID;
     if (c->nfail == 0) return KNN_OK;
     HIPCHK(hipSetDevice(c->device));
-    return knn_launch_rescan_step(c->dtype, c->fail_list, c->nfail, c->qblk, c->q_base,
+    return knn_launch_rescan_step(c->dtype, c->kp, c->fail_list, c->nfail, c->qblk, c->q_base,
                                   d_cblock, c_base, (int)nc, (int)c->n, c->rs_d, c->rs_i,
                                   stream);
 }
@@ -364,7 +399,7 @@ int knn_ctx_rescan_end(knn_ctx_t *c, knn_neighbour_t *d_out, void *stream)
     if (!c || !d_out) return KNN_ERR_INVALID;
     if (c->nfail == 0) return KNN_OK;
     HIPCHK(hipSetDevice(c->device));
-    return knn_launch_rescan_end(c->fail_list, c->nfail, c->rs_d, c->rs_i, c->k, d_out,
+    return knn_launch_rescan_end(c->kp, c->fail_list, c->nfail, c->rs_d, c->rs_i, c->k, d_out,
                                  stream);
 }
 
@@ -393,8 +428,8 @@ int knn_search(const double *X, size_t m, size_t n, int layout, const double *la
                int ngpus, int dtype, knn_neighbour_t *out)
 {
     if (!X || !out || m == 0 || n == 0 || k <= 0) return KNN_ERR_INVALID;
-    if (k > KNN_MAX_K) return KNN_ERR_UNSUPPORTED;
     if (!dtype_ok(dtype)) return KNN_ERR_UNSUPPORTED;
+    if (k > (dtype == KNN_F32 ? KNN_MAX_K_F32 : KNN_MAX_K)) return KNN_ERR_UNSUPPORTED;
     if (layout != KNN_COLMAJOR && layout != KNN_ROWMAJOR) return KNN_ERR_INVALID;
     if (ngpus < 1) return KNN_ERR_INVALID;
     int rc = KNN_OK;

@@ -16,8 +16,10 @@ extern "C" {
 #define KNN_TQ 128        /* queries per workgroup (8 waves x 16)      */
 #define KNN_TC 128        /* corpus rows per tile                      */
 #define KNN_BK 16         /* fp64 features per LDS chunk (128 B a row) */
-#define KNN_KL 16         /* per-lane candidate list capacity          */
+#define KNN_KL 16         /* per-lane candidate list capacity, k <= 32 */
 #define KNN_KP 32         /* per-query state / selection capacity      */
+#define KNN_KL_L 40       /* the same for 32 < k <= 128 (fp32 only):   */
+#define KNN_KP_L 128      /*   P(Bin(100, 1/4) > 40) ~ 3e-4 per lane   */
 #define KNN_ROW_ALIGN 128 /* packed-block row padding                  */
 
 /* meta doubles of a packed block */
@@ -38,6 +40,9 @@ static inline size_t knn_rows_pad(size_t rows) { return knn_round_up(rows ? rows
 static inline size_t knn_n_pad(size_t n) { return knn_round_up(n ? n : 1, KNN_BK); }
 /* element size and padded row length of a packed block of `dtype`
  * (KNN_F64 / KNN_F32): rows are padded to whole 128-byte chunks */
+/* state capacity and per-lane list length serving k */
+static inline int knn_kp_for(int k) { return k <= KNN_KP ? KNN_KP : KNN_KP_L; }
+static inline int knn_kl_for(int kp) { return kp == KNN_KP ? KNN_KL : KNN_KL_L; }
 static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
 {
@@ -48,27 +53,27 @@ static inline size_t knn_n_pad_dt(size_t n, int dtype)
  * KNN_F32); block pointers are untyped device pointers. */
 int knn_launch_pack(void *blk, int dtype, size_t cap, size_t rows, size_t n, const void *src,
                     int src_dtype, size_t ld, int layout, void *stream);
-int knn_launch_dist_topk(int dtype, const void *qblk, size_t q_rows_pad, size_t q_base, int nq,
+int knn_launch_dist_topk(int dtype, int kp, const void *qblk, size_t q_rows_pad, size_t q_base, int nq,
                          const void *cblk, size_t c_rows_pad, size_t c_base, int nc,
                          int n, const double *meta, int nsplit,
                          double *part_d, int *part_i, double *part_T, int nq_pad,
                          double *qthr, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
-int knn_launch_merge(int dtype, const double *part_d, const int *part_i, const double *part_T,
+int knn_launch_merge(int dtype, int kp, const double *part_d, const int *part_i, const double *part_T,
                      int nsplit, int nq, int nq_pad, int first_step,
                      double *st_d, double *st_x, int *st_i, double *st_T,
                      const void *qblk, const void *cblk, size_t c_base, int nc,
                      int n, const double *meta, void *stream);
-int knn_launch_finalize(int dtype, const double *st_d, const double *st_x, const int *st_i,
+int knn_launch_finalize(int dtype, int kp, const double *st_d, const double *st_x, const int *st_i,
                         const double *st_T, const void *qblk, size_t q_rows_pad,
                         int nq, int n, int k, const double *meta,
                         knn_neighbour_t *out, int *fail_count, int *fail_list,
                         int *mode_out, void *stream);
-int knn_launch_rescan_init(double *rs_d, int *rs_i, int nfail, void *stream);
-int knn_launch_rescan_step(int dtype, const int *fail_list, int nfail, const void *qblk,
+int knn_launch_rescan_init(int kp, double *rs_d, int *rs_i, int nfail, void *stream);
+int knn_launch_rescan_step(int dtype, int kp, const int *fail_list, int nfail, const void *qblk,
                            size_t q_base, const void *cblk, size_t c_base, int nc,
                            int n, double *rs_d, int *rs_i, void *stream);
-int knn_launch_rescan_end(const int *fail_list, int nfail, const double *rs_d,
+int knn_launch_rescan_end(int kp, const int *fail_list, int nfail, const double *rs_d,
                           const int *rs_i, int k, knn_neighbour_t *out, void *stream);
 
 #ifdef __cplusplus

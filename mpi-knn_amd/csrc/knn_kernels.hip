@@ -361,7 +361,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     asm volatile("" ::"v"(qn));
     const int nfc = n_pad / BK;
     if constexpr ((ABL & 16) != 0) {
-        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+        if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
     }
 
     T L[KL];
@@ -551,8 +551,13 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // between them the reads `rdj(j)` of the next segment and one staging
     // load `stage()` (sched_barrier-pinned order)
     constexpr int SJ = (ABL & 2048) ? 0 : 2;   // m-tile pair after which a segment's load issues
+    // fp64: an m-tile's two k-steps back to back (measured 1.2% faster than
+    // interleaving); fp32: v_mfma_f32_16x16x4 has a 40-cycle dependent
+    // latency against a 32-cycle issue, so its 4 k-steps go round-robin
+    // over the 4 m-tiles.  ABL bit 5 swaps the two orders.
+    constexpr bool PAIRS = (ES == 8) == ((ABL & 32) == 0);
     auto segment = [&](const frag_t (&f)[4], const frag_t &b, int h, auto &&rdj, auto &&stage) {
-        if constexpr ((ABL & 32) == 0) {
+        if constexpr (PAIRS) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 rdj(j);
@@ -701,8 +706,12 @@ __global__ __launch_bounds__(256) void k_merge(
         Td = fmin(Td, __shfl_xor(Td, off));
     }
 
-    double sd = KNN_INF;
-    int si = -1, ssrc = 0, spos = 0;
+    // state slot r (0..KP-1) is kept by lane r & 63 in its register r >> 6
+    constexpr int NS = (KP + 63) / 64;
+    double sd[NS];
+    int si[NS], ssrc[NS], spos[NS];
+#pragma unroll
+    for (int x = 0; x < NS; x++) { sd[x] = KNN_INF; si[x] = -1; ssrc[x] = 0; spos[x] = 0; }
     for (int r = 0; r <= KP; r++) {
         double wd = hd;
         int wi = hi;
@@ -712,11 +721,16 @@ __global__ __launch_bounds__(256) void k_merge(
         const int wl = __builtin_ctzll(who);
         const int wpos = __shfl(pos, wl);
         if (r < KP) {
-            if (lane == r) {
-                sd = wd;
-                si = wi;
-                ssrc = (wl == nl && !first_step) ? 1 : 0;
-                spos = wpos;
+            if (lane == (r & 63)) {
+#pragma unroll
+                for (int x = 0; x < NS; x++) {
+                    if ((r >> 6) == x) {
+                        sd[x] = wd;
+                        si[x] = wi;
+                        ssrc[x] = (wl == nl && !first_step) ? 1 : 0;
+                        spos[x] = wpos;
+                    }
+                }
             }
         } else {
             Td = fmin(Td, wd);
@@ -729,20 +743,30 @@ __global__ __launch_bounds__(256) void k_merge(
         }
     }
 
-    double sx = sd;
-    if (lane < KP && mode == KNN_MODE_GEMM && si >= 0) {
-        if (ssrc) {
-            sx = st_x[(size_t)q * KP + spos];
-        } else {
-            const int row = (int)((long)si - (long)c_base);
-            sx = knn_exact_sq<TE>(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n);
+    double sx[NS];
+#pragma unroll
+    for (int x = 0; x < NS; x++) {
+        sx[x] = sd[x];
+        if (lane + 64 * x < KP && mode == KNN_MODE_GEMM && si[x] >= 0) {
+            if (ssrc[x]) {
+                sx[x] = st_x[(size_t)q * KP + spos[x]];
+            } else {
+                const int row = (int)((long)si[x] - (long)c_base);
+                sx[x] = knn_exact_sq<TE>(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n);
+            }
         }
     }
-    // all reads of the old state are done (wave-private query) -> overwrite
-    if (lane < KP) {
-        st_d[(size_t)q * KP + lane] = sd;
-        st_x[(size_t)q * KP + lane] = sx;
-        st_i[(size_t)q * KP + lane] = (sd == KNN_INF) ? -1 : si;
+    // every read of the old state (any lane, any slot) completes before the
+    // first write (wave-private query)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int x = 0; x < NS; x++) {
+        const int r = lane + 64 * x;
+        if (r < KP) {
+            st_d[(size_t)q * KP + r] = sd[x];
+            st_x[(size_t)q * KP + r] = sx[x];
+            st_i[(size_t)q * KP + r] = (sd[x] == KNN_INF) ? -1 : si[x];
+        }
     }
     if (lane == 0) { st_T[2 * (size_t)q] = T; st_T[2 * (size_t)q + 1] = Td; }
     (void)nc;
@@ -776,52 +800,98 @@ __global__ __launch_bounds__(256) void k_finalize(
         if (lane == 0) fail_list[atomicAdd(fail_count, 1)] = q;
         return;
     }
-    double sd = KNN_INF, sx = KNN_INF;
-    int si = -1;
-    if (lane < KP) {
-        sd = st_d[(size_t)q * KP + lane];
-        sx = st_x[(size_t)q * KP + lane];
-        si = st_i[(size_t)q * KP + lane];
+    constexpr int NS = (KP + 63) / 64;   // state slot r on lane r & 63, register r >> 6
+    double sd[NS], sx[NS];
+    int si[NS];
+#pragma unroll
+    for (int x = 0; x < NS; x++) {
+        const int r = lane + 64 * x;
+        sd[x] = KNN_INF;
+        sx[x] = KNN_INF;
+        si[x] = -1;
+        if (r < KP) {
+            sd[x] = st_d[(size_t)q * KP + r];
+            sx[x] = st_x[(size_t)q * KP + r];
+            si[x] = st_i[(size_t)q * KP + r];
+        }
     }
     const double T = st_T[2 * (size_t)q], Td = st_T[2 * (size_t)q + 1];
+    const int kl = k - 1;
     if (mode == KNN_MODE_INT) {
         // state is sorted by exact (d^2, idx) and zeros were never admitted.
         // A candidate a lane filter turned away has d^2 >= T; with d^2 == T
         // it may precede the k-th by index, so certify only tau < T.
-        const bool valid = si >= 0 && sd < KNN_INF;
-        const int nnz = __popcll(__ballot(valid));
+        bool valid[NS];
+        int nnz = 0;
+#pragma unroll
+        for (int x = 0; x < NS; x++) {
+            valid[x] = si[x] >= 0 && sd[x] < KNN_INF;
+            nnz += __popcll(__ballot(valid[x]));
+        }
         bool ok;
-        if (nnz >= k) ok = (T == KNN_INF) || (__shfl(sd, k - 1) < T);
-        else ok = (T == KNN_INF);
+        if (nnz >= k) {
+            double tau = KNN_INF;
+#pragma unroll
+            for (int x = 0; x < NS; x++) {
+                const double v = __shfl(sd[x], kl & 63);
+                if ((kl >> 6) == x) tau = v;
+            }
+            ok = (T == KNN_INF) || (tau < T);
+        } else {
+            ok = (T == KNN_INF);
+        }
         if (!ok) {
             if (lane == 0) fail_list[atomicAdd(fail_count, 1)] = q;
             return;
         }
-        if (lane < k) {
-            knn_neighbour_t rec;
-            rec.distance = valid ? sqrt(sd) : KNN_INF;
-            rec.idx = valid ? si + 1 : 0;
-            rec.label = 0;
-            o[lane] = rec;
+#pragma unroll
+        for (int x = 0; x < NS; x++) {
+            const int r = lane + 64 * x;
+            if (r < k) {
+                knn_neighbour_t rec;
+                rec.distance = valid[x] ? sqrt(sd[x]) : KNN_INF;
+                rec.idx = valid[x] ? si[x] + 1 : 0;
+                rec.label = 0;
+                o[r] = rec;
+            }
         }
         return;
     }
     // GEMM mode
-    const bool valid = (si >= 0) && (sx == sx) && (sx != 0.0) && (sx < KNN_INF);
-    const double key = valid ? sqrt(sx) : KNN_INF;
-    const int kid = valid ? si : 0x7fffffff;
-    int rank = 0;
-    for (int j = 0; j < KP; j++) {
-        double kj = __shfl(key, j);
-        int ij = __shfl(kid, j);
-        rank += (kj < key || (kj == key && ij < kid)) ? 1 : 0;
+    bool valid[NS];
+    double key[NS];
+    int kid[NS], rank[NS];
+#pragma unroll
+    for (int x = 0; x < NS; x++) {
+        valid[x] = (si[x] >= 0) && (sx[x] == sx[x]) && (sx[x] != 0.0) && (sx[x] < KNN_INF);
+        key[x] = valid[x] ? sqrt(sx[x]) : KNN_INF;
+        kid[x] = valid[x] ? si[x] : 0x7fffffff;
+        rank[x] = 0;
     }
-    const int nnz = __popcll(__ballot(valid));
+    // rank = number of entries before this one by (sqrt(S), idx); unused
+    // slots (key inf, id max) precede nothing
+    for (int j = 0; j < 64; j++) {
+#pragma unroll
+        for (int y = 0; y < NS; y++) {
+            const double kj = __shfl(key[y], j);
+            const int ij = __shfl(kid[y], j);
+#pragma unroll
+            for (int x = 0; x < NS; x++)
+                rank[x] += (kj < key[x] || (kj == key[x] && ij < kid[x])) ? 1 : 0;
+        }
+    }
+    int nnz = 0;
+#pragma unroll
+    for (int x = 0; x < NS; x++) nnz += __popcll(__ballot(valid[x]));
     const double Tb = fmin(T, Td);
     bool ok;
     if (nnz >= k) {
-        const unsigned long long at = __ballot(valid && rank == k - 1);
-        const double tau = __shfl(sx, __builtin_ctzll(at));
+        double tau = KNN_INF;
+#pragma unroll
+        for (int x = 0; x < NS; x++) {
+            const unsigned long long at = __ballot(valid[x] && rank[x] == kl);
+            if (at) tau = __shfl(sx[x], __builtin_ctzll(at));
+        }
         // E bounds |GEMM-form d^2 - exact S| (unit roundoff of the filter
         // arithmetic: 2^-53 fp64, 2^-24 fp32) plus the reference's own
         const double u = KT<TE>::U;
@@ -834,27 +904,38 @@ __global__ __launch_bounds__(256) void k_finalize(
         if (lane == 0) fail_list[atomicAdd(fail_count, 1)] = q;
         return;
     }
-    if (valid && rank < k) {
-        knn_neighbour_t rec;
-        rec.distance = key;
-        rec.idx = si + 1;
-        rec.label = 0;
-        o[rank] = rec;
-    }
-    if (lane >= nnz && lane < k) {
-        knn_neighbour_t rec;
-        rec.distance = KNN_INF;
-        rec.idx = 0;
-        rec.label = 0;
-        o[lane] = rec;
+#pragma unroll
+    for (int x = 0; x < NS; x++) {
+        if (valid[x] && rank[x] < k) {
+            knn_neighbour_t rec;
+            rec.distance = key[x];
+            rec.idx = si[x] + 1;
+            rec.label = 0;
+            o[rank[x]] = rec;
+        }
+        const int r = lane + 64 * x;
+        if (r >= nnz && r < k) {
+            knn_neighbour_t rec;
+            rec.distance = KNN_INF;
+            rec.idx = 0;
+            rec.label = 0;
+            o[r] = rec;
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
-// Exact rescan (rare path): one workgroup per unresolved query; thread t
-// scans rows t, t+256, ... with the reference's arithmetic and key
-// (distance = sqrt(S), S != 0), keeps a register list, then the 256 lists
-// and the running rescan list are merged by (distance, idx) in LDS.
+// Exact rescan (rare path): one workgroup per unresolved query merges this
+// block's rows into the query's running rescan list (KP entries ordered by
+// (distance, idx); distance = sqrt(S) in the reference's arithmetic,
+// 0 < distance < inf as serial:86 admits).  Thread t scans rows t, t+256,
+// ... and keeps its KT smallest keys above a floor; a block tournament
+// merges the 256 thread lists with the running list.  A thread that saw
+// more than KT candidates may have dropped some, but every candidate with a
+// key <= B (the smallest KT-th key among such threads) is in the lists, so
+// the merge takes entries only up to B; if the list is not full by then,
+// the scan repeats above the last key taken.  Exact for any KP; one pass
+// unless more than KT of this block's KP nearest rows fall to one thread.
 // ---------------------------------------------------------------------------
 template <typename TE, int KP>
 __global__ __launch_bounds__(256) void k_rescan_step(
@@ -862,64 +943,96 @@ __global__ __launch_bounds__(256) void k_rescan_step(
     size_t q_base, const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
     double *__restrict__ rs_d, int *__restrict__ rs_i)
 {
-    __shared__ double sh_d[256 + 1][KP];
-    __shared__ int sh_i[256 + 1][KP];
+    constexpr int KT = 8;
+    __shared__ double sh_d[256][KT];
+    __shared__ int sh_i[256][KT];
+    __shared__ double old_d[KP], new_d[KP];
+    __shared__ int old_i[KP], new_i[KP];
     __shared__ double red_d[4];
-    __shared__ int red_i[4];
+    __shared__ int red_i[4], red_w[4];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int slot = blockIdx.x;
     const int q = fail_list[slot];
     const TE *qa = qblk + (size_t)q * n_pad_q;
-    double L[KP];
-    int I[KP];
-#pragma unroll
-    for (int e = 0; e < KP; e++) { L[e] = KNN_INF; I[e] = 0x7fffffff; }
-    for (int row = tid; row < nc; row += 256) {
-        const double S = knn_exact_sq<TE>(qa, cblk + (size_t)row * n_pad, n);
-        const double d = sqrt(S);
-        if (d != 0.0) list_insert<KP>(L, I, d, (int)(c_base + row));
+    for (int e = tid; e < KP; e += 256) {
+        const double v = rs_d[(size_t)slot * KP + e];
+        old_d[e] = v;
+        old_i[e] = (v == KNN_INF) ? 0x7fffffff : rs_i[(size_t)slot * KP + e];
+        new_d[e] = KNN_INF;
+        new_i[e] = 0x7fffffff;
     }
+    // block-wide minimum of (d, i) carrying its owner w; every thread gets it
+    auto block_min = [&](double &d, int &i, int &w) {
+        for (int off = 32; off > 0; off >>= 1) {
+            const double od = __shfl_xor(d, off);
+            const int oi = __shfl_xor(i, off), ow = __shfl_xor(w, off);
+            const bool take = (od < d) || (od == d && oi < i);
+            d = take ? od : d;
+            i = take ? oi : i;
+            w = take ? ow : w;
+        }
+        if (lane == 0) { red_d[wave] = d; red_i[wave] = i; red_w[wave] = w; }
+        __syncthreads();
+        d = red_d[0];
+        i = red_i[0];
+        w = red_w[0];
+        for (int x = 1; x < 4; x++) {
+            if (red_d[x] < d || (red_d[x] == d && red_i[x] < i)) { d = red_d[x]; i = red_i[x]; w = red_w[x]; }
+        }
+        __syncthreads();
+    };
+    int produced = 0, pos_old = 0;   // block-uniform
+    double fd = -1.0;                // floor key (fd, fi): smaller keys are taken
+    int fi = -1;
+    for (;;) {
+        double L[KT];
+        int I[KT];
 #pragma unroll
-    for (int e = 0; e < KP; e++) {
-        sh_d[tid][e] = L[e];
-        sh_i[tid][e] = (L[e] == KNN_INF) ? 0x7fffffff : I[e];
-    }
-    if (tid < KP) {
-        double v = rs_d[(size_t)slot * KP + tid];
-        sh_d[256][tid] = v;
-        sh_i[256][tid] = (v == KNN_INF) ? 0x7fffffff : rs_i[(size_t)slot * KP + tid];
+        for (int e = 0; e < KT; e++) { L[e] = KNN_INF; I[e] = 0x7fffffff; }
+        int cnt = 0;
+        for (int row = tid; row < nc; row += 256) {
+            const double S = knn_exact_sq<TE>(qa, cblk + (size_t)row * n_pad, n);
+            const double d = sqrt(S);
+            const int id = (int)(c_base + row);
+            if (d != 0.0 && d < KNN_INF && (d > fd || (d == fd && id > fi))) {
+                cnt++;
+                list_insert<KT>(L, I, d, id);   // rows ascend: ties stay in id order
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < KT; e++) {
+            sh_d[tid][e] = L[e];
+            sh_i[tid][e] = (L[e] == KNN_INF) ? 0x7fffffff : I[e];
+        }
+        double Bd = (cnt > KT) ? L[KT - 1] : KNN_INF;
+        int Bi = (cnt > KT) ? I[KT - 1] : 0x7fffffff, bw = 0;
+        block_min(Bd, Bi, bw);           // its barrier also publishes the lists
+        int pos = 0;
+        bool again = false;
+        while (produced < KP) {
+            double hd = (pos < KT) ? sh_d[tid][pos] : KNN_INF;
+            int hi = (pos < KT) ? sh_i[tid][pos] : 0x7fffffff, hw = tid;
+            if (tid == 0 && pos_old < KP) {
+                const double od = old_d[pos_old];
+                const int oi = old_i[pos_old];
+                if (od < hd || (od == hd && oi < hi)) { hd = od; hi = oi; hw = 256; }
+            }
+            block_min(hd, hi, hw);
+            if (hd == KNN_INF) break;                                  // both sources empty
+            if (Bd < hd || (Bd == hd && Bi < hi)) { again = true; break; }  // past B
+            if (tid == 0) { new_d[produced] = hd; new_i[produced] = hi; }
+            produced++;
+            fd = hd;
+            fi = hi;
+            if (hw == 256) pos_old++;
+            else if (tid == hw) pos++;
+        }
+        if (!again) break;
     }
     __syncthreads();
-    // tournament over 257 sorted lists: thread t owns list t (t == 0 also 256)
-    int pos = 0, pos2 = 0;
-    for (int r = 0; r < KP; r++) {
-        double hd = (pos < KP) ? sh_d[tid][pos] : KNN_INF;
-        int hi = (pos < KP) ? sh_i[tid][pos] : 0x7fffffff;
-        if (tid == 0) {
-            double h2 = (pos2 < KP) ? sh_d[256][pos2] : KNN_INF;
-            int i2 = (pos2 < KP) ? sh_i[256][pos2] : 0x7fffffff;
-            if (h2 < hd || (h2 == hd && i2 < hi)) { hd = h2; hi = i2; }
-        }
-        double wd = hd;
-        int wi = hi;
-        wave_argmin(wd, wi);
-        if (lane == 0) { red_d[wave] = wd; red_i[wave] = wi; }
-        __syncthreads();
-        double bd = red_d[0];
-        int bi = red_i[0];
-        for (int w = 1; w < 4; w++) {
-            if (red_d[w] < bd || (red_d[w] == bd && red_i[w] < bi)) { bd = red_d[w]; bi = red_i[w]; }
-        }
-        __syncthreads();
-        if (tid == 0) {
-            rs_d[(size_t)slot * KP + r] = bd;
-            rs_i[(size_t)slot * KP + r] = (bd == KNN_INF) ? -1 : bi;
-        }
-        if (bd != KNN_INF) {
-            // advance whichever list held the winner (indices are unique)
-            if (pos < KP && sh_i[tid][pos] == bi && sh_d[tid][pos] == bd) pos++;
-            else if (tid == 0 && pos2 < KP && sh_i[256][pos2] == bi && sh_d[256][pos2] == bd) pos2++;
-        }
+    for (int e = tid; e < KP; e += 256) {
+        rs_d[(size_t)slot * KP + e] = new_d[e];
+        rs_i[(size_t)slot * KP + e] = (new_d[e] == KNN_INF) ? -1 : new_i[e];
     }
     (void)q_base;
 }
@@ -1001,7 +1114,7 @@ extern "C" int knn_launch_pack(void *blk, int dtype, size_t cap, size_t rows, si
     return KNN_ERR_INVALID;
 }
 
-template <typename T>
+template <typename T, int KL, int KP>
 static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int nq, const T *cblk,
                             size_t c_rows_pad, size_t c_base, int nc, int n, const double *meta,
                             int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
@@ -1018,31 +1131,37 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
         return KNN_ERR_INVALID;
     const T *qnorm = qblk + q_rows_pad * np;
     const T *cnorm = cblk + c_rows_pad * np;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KNN_KL, KNN_KP>), dim3((unsigned)(nqb * nsplit)),
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP>), dim3((unsigned)(nqb * nsplit)),
                        dim3(512), 0, s, qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np,
                        ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
                        (unsigned long long *)qthr);
     return hip_status();
 }
 
-extern "C" int knn_launch_dist_topk(int dtype, const void *qblk, size_t q_rows_pad, size_t q_base,
-                                    int nq, const void *cblk, size_t c_rows_pad, size_t c_base,
-                                    int nc, int n, const double *meta, int nsplit,
+// The served (element type, state capacity) pairs: fp64 k <= 32, fp32 k <= 128.
+#define KNN_DISPATCH(dtype, kp, CALL)                                          \
+    do {                                                                       \
+        if ((dtype) == KNN_F64 && (kp) == KNN_KP) { CALL(double, KNN_KL, KNN_KP); }       \
+        else if ((dtype) == KNN_F32 && (kp) == KNN_KP) { CALL(float, KNN_KL, KNN_KP); }   \
+        else if ((dtype) == KNN_F32 && (kp) == KNN_KP_L) { CALL(float, KNN_KL_L, KNN_KP_L); } \
+        else return KNN_ERR_INVALID;                                           \
+    } while (0)
+
+extern "C" int knn_launch_dist_topk(int dtype, int kp, const void *qblk, size_t q_rows_pad,
+                                    size_t q_base, int nq, const void *cblk, size_t c_rows_pad,
+                                    size_t c_base, int nc, int n, const double *meta, int nsplit,
                                     double *part_d, int *part_i, double *part_T, int nq_pad,
                                     double *qthr, void *stream)
 {
-    if (dtype == KNN_F64)
-        return launch_dist_topk((const double *)qblk, q_rows_pad, q_base, nq, (const double *)cblk,
-                                c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i, part_T,
-                                nq_pad, qthr, (hipStream_t)stream);
-    if (dtype == KNN_F32)
-        return launch_dist_topk((const float *)qblk, q_rows_pad, q_base, nq, (const float *)cblk,
-                                c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i, part_T,
-                                nq_pad, qthr, (hipStream_t)stream);
-    return KNN_ERR_INVALID;
+#define CALL(T, KL, KP)                                                                        \
+    return launch_dist_topk<T, KL, KP>((const T *)qblk, q_rows_pad, q_base, nq, (const T *)cblk, \
+                                       c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i,  \
+                                       part_T, nq_pad, qthr, (hipStream_t)stream)
+    KNN_DISPATCH(dtype, kp, CALL);
+#undef CALL
 }
 
-extern "C" int knn_launch_merge(int dtype, const double *part_d, const int *part_i,
+extern "C" int knn_launch_merge(int dtype, int kp, const double *part_d, const int *part_i,
                                 const double *part_T, int nsplit, int nq, int nq_pad,
                                 int first_step, double *st_d, double *st_x, int *st_i,
                                 double *st_T, const void *qblk, const void *cblk, size_t c_base,
@@ -1052,54 +1171,44 @@ extern "C" int knn_launch_merge(int dtype, const double *part_d, const int *part
     const int np = (int)knn_n_pad_dt(n, dtype);
     const dim3 grid((unsigned)((nq + 3) / 4));
     hipStream_t s = (hipStream_t)stream;
-    if (dtype == KNN_F64)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<double, KNN_KL, KNN_KP>), grid, dim3(256), 0, s,
-                           part_d, part_i, part_T, nsplit, nq, nq_pad, first_step, st_d, st_x,
-                           st_i, st_T, (const double *)qblk, (const double *)cblk, c_base, nc, n,
-                           np, meta);
-    else if (dtype == KNN_F32)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<float, KNN_KL, KNN_KP>), grid, dim3(256), 0, s,
-                           part_d, part_i, part_T, nsplit, nq, nq_pad, first_step, st_d, st_x,
-                           st_i, st_T, (const float *)qblk, (const float *)cblk, c_base, nc, n,
-                           np, meta);
-    else
-        return KNN_ERR_INVALID;
-    return hip_status();
+#define CALL(T, KL, KP)                                                                         \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KL, KP>), grid, dim3(256), 0, s, part_d, part_i, \
+                       part_T, nsplit, nq, nq_pad, first_step, st_d, st_x, st_i, st_T,            \
+                       (const T *)qblk, (const T *)cblk, c_base, nc, n, np, meta);               \
+    return hip_status()
+    KNN_DISPATCH(dtype, kp, CALL);
+#undef CALL
 }
 
-extern "C" int knn_launch_finalize(int dtype, const double *st_d, const double *st_x,
+extern "C" int knn_launch_finalize(int dtype, int kp, const double *st_d, const double *st_x,
                                    const int *st_i, const double *st_T, const void *qblk,
                                    size_t q_rows_pad, int nq, int n, int k, const double *meta,
                                    knn_neighbour_t *out, int *fail_count, int *fail_list,
                                    int *mode_out, void *stream)
 {
-    if (k <= 0 || k > KNN_KP) return KNN_ERR_INVALID;
+    if (k <= 0 || k > kp) return KNN_ERR_INVALID;
     const size_t off = q_rows_pad * knn_n_pad_dt(n, dtype);
     const dim3 grid((unsigned)((nq + 3) / 4));
     hipStream_t s = (hipStream_t)stream;
-    if (dtype == KNN_F64)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_finalize<double, KNN_KP>), grid, dim3(256), 0, s, st_d,
-                           st_x, st_i, st_T, (const double *)qblk + off, nq, n, k, meta, out,
-                           fail_count, fail_list, mode_out);
-    else if (dtype == KNN_F32)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_finalize<float, KNN_KP>), grid, dim3(256), 0, s, st_d,
-                           st_x, st_i, st_T, (const float *)qblk + off, nq, n, k, meta, out,
-                           fail_count, fail_list, mode_out);
-    else
-        return KNN_ERR_INVALID;
-    return hip_status();
+#define CALL(T, KL, KP)                                                                        \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_finalize<T, KP>), grid, dim3(256), 0, s, st_d, st_x,   \
+                       st_i, st_T, (const T *)qblk + off, nq, n, k, meta, out, fail_count,       \
+                       fail_list, mode_out);                                                     \
+    return hip_status()
+    KNN_DISPATCH(dtype, kp, CALL);
+#undef CALL
 }
 
-extern "C" int knn_launch_rescan_init(double *rs_d, int *rs_i, int nfail, void *stream)
+extern "C" int knn_launch_rescan_init(int kp, double *rs_d, int *rs_i, int nfail, void *stream)
 {
-    const int cnt = nfail * KNN_KP;
+    const int cnt = nfail * kp;
     if (cnt <= 0) return KNN_OK;
     hipLaunchKernelGGL(k_rescan_init, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, rs_d, rs_i, cnt);
     return hip_status();
 }
 
-extern "C" int knn_launch_rescan_step(int dtype, const int *fail_list, int nfail,
+extern "C" int knn_launch_rescan_step(int dtype, int kp, const int *fail_list, int nfail,
                                       const void *qblk, size_t q_base, const void *cblk,
                                       size_t c_base, int nc, int n, double *rs_d, int *rs_i,
                                       void *stream)
@@ -1107,25 +1216,21 @@ extern "C" int knn_launch_rescan_step(int dtype, const int *fail_list, int nfail
     if (nfail <= 0) return KNN_OK;
     const int np = (int)knn_n_pad_dt(n, dtype);
     hipStream_t s = (hipStream_t)stream;
-    if (dtype == KNN_F64)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_step<double, KNN_KP>), dim3((unsigned)nfail),
-                           dim3(256), 0, s, fail_list, (const double *)qblk, np, q_base,
-                           (const double *)cblk, c_base, nc, n, np, rs_d, rs_i);
-    else if (dtype == KNN_F32)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_step<float, KNN_KP>), dim3((unsigned)nfail),
-                           dim3(256), 0, s, fail_list, (const float *)qblk, np, q_base,
-                           (const float *)cblk, c_base, nc, n, np, rs_d, rs_i);
-    else
-        return KNN_ERR_INVALID;
-    return hip_status();
+#define CALL(T, KL, KP)                                                                         \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_step<T, KP>), dim3((unsigned)nfail), dim3(256), 0, \
+                       s, fail_list, (const T *)qblk, np, q_base, (const T *)cblk, c_base, nc, n,  \
+                       np, rs_d, rs_i);                                                           \
+    return hip_status()
+    KNN_DISPATCH(dtype, kp, CALL);
+#undef CALL
 }
 
-extern "C" int knn_launch_rescan_end(const int *fail_list, int nfail, const double *rs_d,
+extern "C" int knn_launch_rescan_end(int kp, const int *fail_list, int nfail, const double *rs_d,
                                      const int *rs_i, int k, knn_neighbour_t *out, void *stream)
 {
     const int cnt = nfail * k;
     if (cnt <= 0) return KNN_OK;
     hipLaunchKernelGGL(k_rescan_end, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, fail_list, nfail, KNN_KP, rs_d, rs_i, k, out);
+                       (hipStream_t)stream, fail_list, nfail, kp, rs_d, rs_i, k, out);
     return hip_status();
 }

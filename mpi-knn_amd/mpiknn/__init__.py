@@ -28,7 +28,8 @@ OK, ERR_INVALID, ERR_NOMEM, ERR_HIP, ERR_IO, ERR_FORMAT, ERR_UNSUPPORTED, ERR_NO
 COLMAJOR, ROWMAJOR = 0, 1
 F64, F32 = 0, 1
 VOTE_SERIAL, VOTE_MPI, VOTE_MAJORITY = 0, 1, 2
-MAX_K = 32
+MAX_K = 32          # KNN_MAX_K (fp64)
+MAX_K_F32 = 128     # KNN_MAX_K_F32
 META_DOUBLES = 8
 MODE_NAMES = {0: "int-exact", 1: "gemm+rerank", 2: "exact-scan"}
 

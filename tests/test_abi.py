@@ -52,6 +52,12 @@ def test_invalid_arguments(knn):
     assert lib.knn_search(p, 4, 2, 7, None, 3, 1, 0, o) == knn.ERR_INVALID
     assert lib.knn_search(p, 4, 2, 1, None, 33, 1, 0, o) == knn.ERR_UNSUPPORTED
     assert lib.knn_search(p, 4, 2, 1, None, 3, 1, 2, o) == knn.ERR_UNSUPPORTED  # no such dtype
+    # k limits: fp64 32, fp32 128 (include/knn.h KNN_MAX_K / KNN_MAX_K_F32)
+    assert lib.knn_search(p, 4, 2, 1, None, 129, 1, 1, o) == knn.ERR_UNSUPPORTED
+    assert lib.knn_ctx_create_dt(ctypes.byref(h := ctypes.c_void_p()), 0, 4, 2, 4, 33, 0) \
+        == knn.ERR_INVALID
+    assert lib.knn_ctx_create_dt(ctypes.byref(h), 0, 4, 2, 4, 129, 1) == knn.ERR_INVALID
+    assert knn.MAX_K == 32 and knn.MAX_K_F32 == 128
     assert lib.knn_search(p, 4, 2, 1, None, 3, 0, 0, o) == knn.ERR_INVALID
     h = ctypes.c_void_p()
     assert lib.knn_ctx_create(ctypes.byref(h), 0, 0, 2, 4, 3) == knn.ERR_INVALID

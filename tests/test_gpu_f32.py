@@ -115,13 +115,45 @@ def test_f32_nonfinite_scan(knn, oracle):
     assert_same(got, oracle.knn(rounded(X), 30), "nan/inf f32")
 
 
-def test_f32_ring_blocks(knn, oracle):
+@pytest.mark.parametrize("what,k", [("gist_like", 100), ("sift_like", 64), ("gaussian", 128),
+                                    ("gist_like", 31), ("mnist_like", 100), ("binary", 100)])
+def test_f32_large_k(knn, oracle, what, k):
+    """k > 32 (BASELINE configs[4]: k = 100) -- the 128-slot state and the
+    40-deep per-lane lists; every engine mode."""
+    if what == "gist_like":
+        X = datasets.gist_like(1500, 960, clusters=24, seed=k)
+    elif what == "sift_like":
+        X = datasets.sift_like(2500, 128, clusters=32, seed=7)   # fp32 INT mode
+    elif what == "mnist_like":
+        X = datasets.mnist_like(1300, 784, seed=4)[0]            # GEMM, integers
+    elif what == "binary":
+        X = np.random.default_rng(9).integers(0, 2, (900, 10)).astype(np.float64)  # ties
+    else:
+        X = np.random.default_rng(12).normal(0, 1, (1800, 72))
+    got, mode, u = run_engine(X, k)
+    if what == "sift_like":
+        assert mode == 0
+    assert_same(got, oracle.knn(rounded(X), k), "%s f32 k=%d" % (what, k))
+    print("%s k=%d: mode %d, %d rescanned" % (what, k, mode, u))
+
+
+def test_f32_k_exceeds_m(knn, oracle):
+    # fewer points than k: missing slots {INFINITY, 0, 0}
+    X = datasets.gist_like(70, 40, clusters=4, seed=1)
+    got, _ = knn.search(X, 100, dtype="f32")
+    ref = oracle.knn(rounded(X), 100)
+    assert_same(got, ref, "m < k f32")
+    assert np.isinf(got["distance"][:, 69:]).all() and (got["idx"][:, 69:] == 0).all()
+
+
+@pytest.mark.parametrize("k", [30, 100])
+def test_f32_ring_blocks(knn, oracle, k):
     """fp32 blocks rotated as in the ring (simulated on one GPU, P = 3)."""
     import torch
     import mpiknn.ring as ring
     X = datasets.gist_like(1000, 300, clusters=16, seed=3)
     m, n = X.shape
-    full = oracle.knn(rounded(X), 30)
+    full = oracle.knn(rounded(X), k)
     dev = torch.device("cuda", 0)
     Xd = torch.from_numpy(X).to(dev)
     P = 3
@@ -129,7 +161,7 @@ def test_f32_ring_blocks(knn, oracle):
     engines = []
     for g in range(P):
         base, rows = blocks[g]
-        e = ring.GpuEngine(torch, 0, n, R, rows, 30, dtype="f32")
+        e = ring.GpuEngine(torch, 0, n, R, rows, k, dtype="f32")
         e.pack(Xd[base:base + rows].float(), layout_col=False)   # fp32 source
         engines.append(e)
     meta = torch.stack([e.meta for e in engines]).max(dim=0).values
