@@ -1,15 +1,21 @@
 #!/usr/bin/env python3
 """bench.py -- all-kNN queries/sec on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]/[2]): all-kNN, k = 30, fp64, over an
-MNIST-784-shaped corpus of m = 60000 rows (synthetic integer pixels 0..255 --
-no dataset can be fetched; see mpiknn/synth.py), leave-one-out (exact zero
-distances excluded) like knn-serial.c:72-93.  One "step" = one full all-kNN
-pass with the corpus already resident in HBM (column-major, the .mat layout):
-pack -> ring of P corpus blocks (k_dist_topk + k_merge per block) -> finalize
-(+ exact rescan if any query needs it).  value = m / step time (whole job).
+Workload (default, BASELINE.json configs[1]/[2]): all-kNN, k = 30, fp64,
+over an MNIST-784-shaped corpus of m = 60000 rows (synthetic integer pixels
+0..255 -- no dataset can be fetched; see mpiknn/synth.py), leave-one-out
+(exact zero distances excluded) like knn-serial.c:72-93.  One "step" = one
+full all-kNN pass with the corpus already resident in HBM (column-major, the
+.mat layout): pack -> ring of P corpus blocks (k_dist_topk + k_merge per
+block) -> finalize (+ exact rescan if any query needs it).
+value = m / step time (whole job).
 
-  python bench.py [--gpus N --steps K --warmup W]
+--workload sift: configs[3], 1M x 128 fp32 k = 32 (SIFT-like integers,
+row-major fvecs layout).  --workload gist: configs[4]'s shape, n = 960 fp32
+k = 100, with m = 500000 by default (configs[4] is 4M rows on 8 GPUs; pass
+--m 4000000 for the full size).  Both run the fp32 path (include/knn.h).
+
+  python bench.py [--gpus N --steps K --warmup W] [--workload mnist|sift|gist]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 N > 1: one process per GPU, RCCL (torch.distributed "nccl") ring of corpus
@@ -27,6 +33,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpi-knn_amd"))
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix (spec; 78.2 measured, tools/probe)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix (spec, MI355X_MICROARCH.md; 155 measured)
+
+WORKLOADS = {
+    # name: (m, n, k, dtype, layout_col, description)
+    "mnist": (60000, 784, 30, "f64", True,
+              "all-kNN MNIST-784 k=%d (configs[1]: %dx%d fp64, leave-one-out)"),
+    "sift": (1_000_000, 128, 32, "f32", False,
+             "all-kNN SIFT-like k=%d (configs[3]: %dx%d fp32, integer-valued)"),
+    "gist": (500_000, 960, 100, "f32", False,
+             "all-kNN GIST-like k=%d (configs[4] shape: %dx%d fp32, real-valued)"),
+}
 
 
 def cpu_baseline(X, k, budget_s):
@@ -54,9 +71,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--m", type=int, default=60000)
-    ap.add_argument("--n", type=int, default=784)
-    ap.add_argument("--k", type=int, default=30)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mnist")
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", type=int, default=8, help="queries re-checked against the oracle")
@@ -76,20 +94,33 @@ def main():
 
     import mpiknn
     import mpiknn.ring as ring
-    from mpiknn.synth import mnist_like
+    from mpiknn import synth
 
-    m, n, k = args.m, args.n, args.k
-    X, y = mnist_like(m, n)
+    m0, n0, k0, dtype, layout_col, wdesc = WORKLOADS[args.workload]
+    m = args.m or m0
+    n = args.n or n0
+    k = args.k or k0
+    if args.workload == "mnist":
+        X, _ = synth.mnist_like(m, n)
+        data = "synthetic (MNIST-784 shape, integer pixels 0..255, seed 1234)"
+    elif args.workload == "sift":
+        X = synth.sift_like(m, n)
+        data = "synthetic (SIFT-like: 1024-centre mixture, integers 0..255, fp32)"
+    else:
+        X = synth.gist_like(m, n)
+        data = "synthetic (GIST-like: 256-centre mixture in [0,1), fp32)"
     R, blocks = ring.partition(m, P)
     base, rows = blocks[rank]
     dev = torch.device("cuda", local)
-    # own rows, column-major on the device (the .mat layout, serial:82)
-    raw_t = torch.from_numpy(np.ascontiguousarray(X[base:base + rows].T)).to(dev)
-    raw = raw_t.t()
-    engine = ring.GpuEngine(torch, local, n, R, rows, k)
+    if layout_col:
+        # own rows, column-major on the device (the .mat layout, serial:82)
+        raw = torch.from_numpy(np.ascontiguousarray(X[base:base + rows].T)).to(dev).t()
+    else:
+        raw = torch.from_numpy(np.ascontiguousarray(X[base:base + rows])).to(dev)
+    engine = ring.GpuEngine(torch, local, n, R, rows, k, dtype=dtype)
 
     def step():
-        engine.pack(raw, layout_col=True)
+        engine.pack(raw, layout_col=layout_col)
         return ring.ring_search(dist, torch, engine, rank, P, m, base)
 
     def barrier():
@@ -98,14 +129,25 @@ def main():
             dist.barrier(device_ids=[local])
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    last = [time.perf_counter()]
+
+    def progress(what):
+        # keeps long runs visibly alive (stderr, rank 0, at most every 20 s)
+        now = time.perf_counter()
+        if rank == 0 and now - last[0] > 20.0:
+            print("[bench] %s" % what, file=sys.stderr, flush=True)
+            last[0] = now
+
+    for i in range(args.warmup):
         step()
+        progress("warmup %d/%d" % (i + 1, args.warmup))
     engine.ctx.profile(1)
     unresolved = 0
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         unresolved += step()
+        progress("step %d/%d" % (i + 1, args.steps))
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -121,7 +163,8 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         got = engine.result()[: args.check]
-        ref = oracle.knn(X, k, rows=(base, min(args.check, rows)))
+        # the fp32 path is exact on the fp32 points (X is already fp32 there)
+        ref = oracle.knn(X.astype(np.float64, copy=False), k, rows=(base, min(args.check, rows)))
         mism = int((got["idx"] != ref["idx"]).sum() +
                    (got["distance"].view(np.uint64) != ref["distance"].view(np.uint64)).sum())
         check = {"queries": int(len(ref)), "mismatches": mism}
@@ -140,17 +183,18 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        key = "m%d_n%d_p%d" % (m, n, P)
+        key = "m%d_n%d_p%d" % (m, n, P) + ("" if dtype == "f64" else "_" + dtype)
         traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
+    peak = FP64_MFMA_PEAK_TFLOPS if dtype == "f64" else FP32_MFMA_PEAK_TFLOPS
     roofline = {
         "kernel": "k_dist_topk",
         "bound": "mfma",
         "achieved": achieved,
-        "peak": FP64_MFMA_PEAK_TFLOPS,
+        "peak": peak,
         "unit": "TFLOP/s",
-        "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
+        "frac": (achieved / peak) if achieved else None,
         "traffic": traffic,
         "avg_launch_ms": dist_ms / max(launches, 1),
         "launches": launches,
@@ -167,10 +211,10 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic (MNIST-784 shape, integer pixels 0..255, seed 1234)",
-        "config": {"workload": "all-kNN MNIST-784 k=%d (configs[1]: %dx%d fp64, leave-one-out)" % (k, m, n),
-                   "m": m, "n": n, "k": k, "parallelism": "ring%d" % P},
+        "dtype": dtype,
+        "data": data,
+        "config": {"workload": wdesc % (k, m, n), "m": m, "n": n, "k": k,
+                   "parallelism": "ring%d" % P},
         "engine": {"mode": mpiknn.MODE_NAMES.get(mode, str(mode)), "splits": splits,
                    "unresolved_queries": unresolved},
         "check": check,
@@ -178,7 +222,7 @@ def main():
         "cpu_baseline": None,
     }
     if P == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(X, k, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(X.astype(np.float64, copy=False), k, args.cpu_seconds)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

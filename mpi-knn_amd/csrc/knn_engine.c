@@ -48,6 +48,7 @@ struct knn_ctx {
     int *st_i;
     /* unresolved queries */
     int *fail_count, *fail_list, *mode_dev;
+    double *fbound;     /* per query: rescan bound on the k-th key (k_finalize) */
     double *rs_d;
     int *rs_i;
     size_t rs_cap;
@@ -136,6 +137,7 @@ static void ctx_free_buffers(knn_ctx_t *c)
     hipFree(c->st_i);
     hipFree(c->fail_count);
     hipFree(c->fail_list);
+    hipFree(c->fbound);
     hipFree(c->mode_dev);
     hipFree(c->rs_d);
     hipFree(c->rs_i);
@@ -218,6 +220,7 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     ok &= hipMalloc((void **)&c->st_T, np * 2 * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->fail_count, sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->fail_list, np * sizeof(int)) == hipSuccess;
+    ok &= hipMalloc((void **)&c->fbound, np * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->mode_dev, sizeof(int)) == hipSuccess;
     if (!ok) {
         ctx_free_buffers(c);
@@ -337,7 +340,7 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
         ev = &c->prof_ev[3 * c->prof_pending++];
         HIPCHK(hipEventRecord(ev[0], (hipStream_t)stream));
     }
-    RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
+    RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
                               c->part_d, c->part_i, c->part_T, (int)c->nq_pad, c->qthr, stream));
     if (ev) HIPCHK(hipEventRecord(ev[1], (hipStream_t)stream));
@@ -356,7 +359,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     hipStream_t s = (hipStream_t)stream;
     RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
                              (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
-                             c->fail_list, c->mode_dev, stream));
+                             c->fail_list, c->mode_dev, c->fbound, stream));
     int host[2];
     HIPCHK(hipMemcpyAsync(&host[0], c->fail_count, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&host[1], c->mode_dev, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -389,8 +392,8 @@ int knn_ctx_rescan_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_
     if (!c || !d_cblock || nc == 0) return KNN_ERR_INVALID;
     if (c->nfail == 0) return KNN_OK;
     HIPCHK(hipSetDevice(c->device));
-    return knn_launch_rescan_step(c->dtype, c->kp, c->fail_list, c->nfail, c->qblk, c->q_base,
-                                  d_cblock, c_base, (int)nc, (int)c->n, c->rs_d, c->rs_i,
+    return knn_launch_rescan_step(c->dtype, c->kp, c->fail_list, c->nfail, c->fbound, c->qblk,
+                                  d_cblock, c_base, (int)nc, (int)c->n, c->k, c->rs_d, c->rs_i,
                                   stream);
 }
 

@@ -53,7 +53,7 @@ static inline size_t knn_n_pad_dt(size_t n, int dtype)
  * KNN_F32); block pointers are untyped device pointers. */
 int knn_launch_pack(void *blk, int dtype, size_t cap, size_t rows, size_t n, const void *src,
                     int src_dtype, size_t ld, int layout, void *stream);
-int knn_launch_dist_topk(int dtype, int kp, const void *qblk, size_t q_rows_pad, size_t q_base, int nq,
+int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_rows_pad, size_t q_base, int nq,
                          const void *cblk, size_t c_rows_pad, size_t c_base, int nc,
                          int n, const double *meta, int nsplit,
                          double *part_d, int *part_i, double *part_T, int nq_pad,
@@ -68,11 +68,12 @@ int knn_launch_finalize(int dtype, int kp, const double *st_d, const double *st_
                         const double *st_T, const void *qblk, size_t q_rows_pad,
                         int nq, int n, int k, const double *meta,
                         knn_neighbour_t *out, int *fail_count, int *fail_list,
-                        int *mode_out, void *stream);
+                        int *mode_out, double *fbound, void *stream);
 int knn_launch_rescan_init(int kp, double *rs_d, int *rs_i, int nfail, void *stream);
-int knn_launch_rescan_step(int dtype, int kp, const int *fail_list, int nfail, const void *qblk,
-                           size_t q_base, const void *cblk, size_t c_base, int nc,
-                           int n, double *rs_d, int *rs_i, void *stream);
+int knn_launch_rescan_step(int dtype, int kp, const int *fail_list, int nfail,
+                           const double *fbound, const void *qblk, const void *cblk,
+                           size_t c_base, int nc, int n, int k, double *rs_d, int *rs_i,
+                           void *stream);
 int knn_launch_rescan_end(int kp, const int *fail_list, int nfail, const double *rs_d,
                           const int *rs_i, int k, knn_neighbour_t *out, void *stream);
 

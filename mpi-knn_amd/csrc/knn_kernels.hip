@@ -335,7 +335,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const T *__restrict__ cblk, const T *__restrict__ cnorm, size_t c_base, int nc,
     int n, int n_pad, int ntiles, int nsplit, int nqb, const double *__restrict__ meta,
     double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T,
-    int nq_pad, unsigned long long *__restrict__ qthr)
+    int nq_pad, unsigned long long *__restrict__ qthr, int uj)
 {
     constexpr int NST = KNN_NST;
     constexpr int BK = knn_bk<T>();                   // features per 128-B chunk
@@ -360,6 +360,10 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // a vmcnt(0) from hipcc that drains the staging ring once per tile
     asm volatile("" ::"v"(qn));
     const int nfc = n_pad / BK;
+    // lane list slot behind the shared bound: INT mode k+1 candidates (exact
+    // keys, tightest filter); GEMM mode the whole state (slack for the
+    // certificate's error margin)
+    const int ujm = (mode == KNN_MODE_INT) ? (uj & 255) : (uj >> 8);
     if constexpr ((ABL & 16) != 0) {
         if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
     }
@@ -370,7 +374,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     for (int e = 0; e < KL; e++) { L[e] = KNN_INF; I[e] = -1; }
     // Shared per-query bound across splits and ring steps (qthr, bits of a
     // non-negative double, atomicMin).  Any split's thr bounds the query's
-    // KS-th candidate over ALL rows (>= KS distinct candidates lie below
+    // (k+1)-th candidate over ALL rows (>= k+1 distinct candidates lie below
     // it), so a split may start filtering at the smallest bound published so
     // far.  Every value ever stored is a valid bound, so a stale read only
     // costs filter strength; the returning atomic reads it at the memory
@@ -524,9 +528,11 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         for (int mt = 0; mt < 8; mt++) acc[mt] = (acc_t){0, 0, 0, 0};
         if (!any) return;
         // shared threshold of the query's 4 lanes: their union holds
-        // >= KS entries <= max_h L_h[KS/4-1], and every lane already
-        // rejects >= min_h L_h[KL-1]
-        T lmin = L[KL - 1], u = L[KS / 4 - 1];
+        // >= 4(ujm+1) >= k+1 entries <= max_h L_h[ujm], and every lane
+        // already rejects >= min_h L_h[KL-1]
+        T lmin = L[KL - 1], u = L[0];
+#pragma unroll
+        for (int e = 1; e < KL; e++) u = (e == ujm) ? L[e] : u;
         lmin = fmin(lmin, __shfl_xor(lmin, 16));
         lmin = fmin(lmin, __shfl_xor(lmin, 32));
         u = fmax(u, __shfl_xor(u, 16));
@@ -638,6 +644,17 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // no LDS-DMA left in flight
     }
 
+    // INT mode, exact d^2: if no lane's list ends at thr, nothing equal to
+    // thr was ever turned away (the filter rejects only d^2 > thr, and a
+    // full list only what ranks after its last entry), so every rejected
+    // candidate has d^2 >= next(thr).  Publishing that lets the certificate
+    // accept a k-th entry equal to thr -- on integer data with the top k
+    // split evenly over the 4 lanes, thr IS the k-th value.
+    T lastmin = L[KL - 1];
+    lastmin = fmin(lastmin, __shfl_xor(lastmin, 16));
+    lastmin = fmin(lastmin, __shfl_xor(lastmin, 32));
+    T pub = thr;
+    if (mode == KNN_MODE_INT && lastmin > thr && thr < (T)KNN_INF) pub = nextafter(thr, (T)KNN_INF);
     if (myq < nq) {
         const size_t base = (((size_t)split * nq_pad + myq) * 4 + g) * KL;
 #pragma unroll
@@ -646,7 +663,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             part_i[base + e] = I[e];
         }
         if (g == 0) {
-            part_T[(size_t)split * nq_pad + myq] = (double)thr;
+            part_T[(size_t)split * nq_pad + myq] = (double)pub;
             if (qthr != nullptr && thr < (T)KNN_INF)
                 atomicMin(qthr + myq, (unsigned long long)__double_as_longlong((double)thr));
         }
@@ -787,7 +804,8 @@ __global__ __launch_bounds__(256) void k_finalize(
     const int *__restrict__ st_i, const double *__restrict__ st_T,
     const TE *__restrict__ qnorm, int nq, int n, int k,
     const double *__restrict__ meta, knn_neighbour_t *__restrict__ out,
-    int *__restrict__ fail_count, int *__restrict__ fail_list, int *__restrict__ mode_out)
+    int *__restrict__ fail_count, int *__restrict__ fail_list, int *__restrict__ mode_out,
+    double *__restrict__ fbound)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + wave;
@@ -797,7 +815,10 @@ __global__ __launch_bounds__(256) void k_finalize(
     knn_neighbour_t *o = out + (size_t)q * k;
 
     if (mode == KNN_MODE_SCAN) {
-        if (lane == 0) fail_list[atomicAdd(fail_count, 1)] = q;
+        if (lane == 0) {
+            fail_list[atomicAdd(fail_count, 1)] = q;
+            fbound[q] = KNN_INF;
+        }
         return;
     }
     constexpr int NS = (KP + 63) / 64;   // state slot r on lane r & 63, register r >> 6
@@ -829,8 +850,8 @@ __global__ __launch_bounds__(256) void k_finalize(
             nnz += __popcll(__ballot(valid[x]));
         }
         bool ok;
+        double tau = KNN_INF;   // k-th exact d^2 kept: the rescan's bound
         if (nnz >= k) {
-            double tau = KNN_INF;
 #pragma unroll
             for (int x = 0; x < NS; x++) {
                 const double v = __shfl(sd[x], kl & 63);
@@ -841,7 +862,10 @@ __global__ __launch_bounds__(256) void k_finalize(
             ok = (T == KNN_INF);
         }
         if (!ok) {
-            if (lane == 0) fail_list[atomicAdd(fail_count, 1)] = q;
+            if (lane == 0) {
+                fail_list[atomicAdd(fail_count, 1)] = q;
+                fbound[q] = sqrt(tau);
+            }
             return;
         }
 #pragma unroll
@@ -885,23 +909,33 @@ __global__ __launch_bounds__(256) void k_finalize(
     for (int x = 0; x < NS; x++) nnz += __popcll(__ballot(valid[x]));
     const double Tb = fmin(T, Td);
     bool ok;
+    double tau = KNN_INF;   // exact S of the k-th kept: the rescan's bound
     if (nnz >= k) {
-        double tau = KNN_INF;
 #pragma unroll
         for (int x = 0; x < NS; x++) {
             const unsigned long long at = __ballot(valid[x] && rank[x] == kl);
             if (at) tau = __shfl(sx[x], __builtin_ctzll(at));
         }
-        // E bounds |GEMM-form d^2 - exact S| (unit roundoff of the filter
-        // arithmetic: 2^-53 fp64, 2^-24 fp32) plus the reference's own
+        // E bounds |GEMM-form d^2 - exact S| plus the reference's own
+        // rounding, for any candidate c (|c|^2 <= maxnorm):
+        //   fp32 filter: fma-chain dot  gamma_n (|q|^2+|c|^2), norm
+        //   roundings and the two final roundings 4u (|q|^2+|c|^2), times
+        //   (1 + 2(n+4)u) for the second-order terms; the reference's fp64
+        //   S: 4(n+2) 2^-53 (|q|^2+|c|^2).
+        //   fp64 filter: both at u = 2^-53, 8(n+4)u (|q|^2+|c|^2).
         const double u = KT<TE>::U;
-        const double E = 8.0 * (n + 4) * u * ((double)qnorm[q] + meta[KNN_META_MAXNORM]);
+        const double nn = (double)n + 4.0, qc = (double)qnorm[q] + meta[KNN_META_MAXNORM];
+        const double E = (sizeof(TE) == 8) ? 8.0 * nn * u * qc
+                                           : nn * qc * (u * (1.0 + 2.0 * nn * u) + 4.0 * 1.1102230246251565e-16);
         ok = (Tb == KNN_INF) || ((Tb - E) > tau * (1.0 + 1.7763568394002505e-15));
     } else {
         ok = (Tb == KNN_INF);
     }
     if (!ok) {
-        if (lane == 0) fail_list[atomicAdd(fail_count, 1)] = q;
+        if (lane == 0) {
+            fail_list[atomicAdd(fail_count, 1)] = q;
+            fbound[q] = sqrt(tau);
+        }
         return;
     }
 #pragma unroll
@@ -925,116 +959,175 @@ __global__ __launch_bounds__(256) void k_finalize(
 }
 
 // ---------------------------------------------------------------------------
-// Exact rescan (rare path): one workgroup per unresolved query merges this
-// block's rows into the query's running rescan list (KP entries ordered by
-// (distance, idx); distance = sqrt(S) in the reference's arithmetic,
-// 0 < distance < inf as serial:86 admits).  Thread t scans rows t, t+256,
-// ... and keeps its KT smallest keys above a floor; a block tournament
-// merges the 256 thread lists with the running list.  A thread that saw
-// more than KT candidates may have dropped some, but every candidate with a
-// key <= B (the smallest KT-th key among such threads) is in the lists, so
-// the merge takes entries only up to B; if the list is not full by then,
-// the scan repeats above the last key taken.  Exact for any KP; one pass
-// unless more than KT of this block's KP nearest rows fall to one thread.
+// Exact rescan (uncertified queries): the reference's arithmetic on every
+// (query, row) pair -- S = S + (a-b)^2 in j order in fp64, key sqrt(S),
+// 0 < key < inf as serial:86 admits -- merged into the query's running
+// rescan list (its first k entries ordered by (key, idx)).
+//
+// A 256-thread workgroup takes 16 queries, 4 per wave.  The wave's 4 query
+// rows are wave-uniform, so hipcc reads them with scalar loads into SGPRs;
+// lane l streams rows l, l+64, ... with 16-byte loads and accumulates all 4
+// S in registers, so each row is read once per 4 queries (and the 4 waves
+// walk the rows in step, sharing L2/L1 lines).  Zero padding past n adds
+// (0-0)^2 = 0, leaving S bit-identical, so the loop runs to a whole 16 B.
+//
+// Filter: only keys <= dcut can reach the top k, dcut = min(the bound
+// k_finalize left in fbound (the k-th key of the uncertified state: k real
+// candidates lie at or below it), the k-th key of the running list).  Each
+// lane keeps its KT smallest admitted keys above a floor; the merge (wave
+// argmin rounds, one query at a time) takes entries only up to B, the
+// smallest KT-th key of any lane that dropped one, and if the list is not
+// complete by then the wave scans again above the last key taken.
 // ---------------------------------------------------------------------------
 template <typename TE, int KP>
 __global__ __launch_bounds__(256) void k_rescan_step(
-    const int *__restrict__ fail_list, const TE *__restrict__ qblk, int n_pad_q,
-    size_t q_base, const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
-    double *__restrict__ rs_d, int *__restrict__ rs_i)
+    const int *__restrict__ fail_list, int nfail, const double *__restrict__ fbound,
+    const TE *__restrict__ qblk, int n_pad_q, const TE *__restrict__ cblk, size_t c_base,
+    int nc, int n, int n_pad, int k, double *__restrict__ rs_d, int *__restrict__ rs_i)
 {
-    constexpr int KT = 8;
-    __shared__ double sh_d[256][KT];
-    __shared__ int sh_i[256][KT];
-    __shared__ double old_d[KP], new_d[KP];
-    __shared__ int old_i[KP], new_i[KP];
-    __shared__ double red_d[4];
-    __shared__ int red_i[4], red_w[4];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int slot = blockIdx.x;
-    const int q = fail_list[slot];
-    const TE *qa = qblk + (size_t)q * n_pad_q;
-    for (int e = tid; e < KP; e += 256) {
-        const double v = rs_d[(size_t)slot * KP + e];
-        old_d[e] = v;
-        old_i[e] = (v == KNN_INF) ? 0x7fffffff : rs_i[(size_t)slot * KP + e];
-        new_d[e] = KNN_INF;
-        new_i[e] = 0x7fffffff;
+#pragma clang fp contract(off)
+    constexpr int KT = 4, QW = 4;
+    constexpr int V = 16 / (int)sizeof(TE);          // elements per 16-byte load
+    constexpr int NS = (KP + 63) / 64;                // list slot r: lane r & 63, reg r >> 6
+    typedef typename std::conditional<sizeof(TE) == 8, dbl2, flt4>::type vec_t;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int slot0 = blockIdx.x * 16 + wave * QW;
+    if (slot0 >= nfail) return;                       // wave-uniform
+    const int nr = (n + V - 1) / V;                   // 16-byte pieces per row
+
+    const TE *qp[QW];
+    double dcut[QW];
+    int slot[QW];
+    bool done[QW];
+#pragma unroll
+    for (int x = 0; x < QW; x++) {
+        slot[x] = slot0 + x;
+        done[x] = slot[x] >= nfail;
+        const int q = done[x] ? fail_list[slot0] : fail_list[slot[x]];
+        qp[x] = qblk + (size_t)q * n_pad_q;
+        const double kth = rs_d[(size_t)(done[x] ? slot0 : slot[x]) * KP + (k - 1)];
+        dcut[x] = fmin(fbound[q], kth);
     }
-    // block-wide minimum of (d, i) carrying its owner w; every thread gets it
-    auto block_min = [&](double &d, int &i, int &w) {
-        for (int off = 32; off > 0; off >>= 1) {
-            const double od = __shfl_xor(d, off);
-            const int oi = __shfl_xor(i, off), ow = __shfl_xor(w, off);
-            const bool take = (od < d) || (od == d && oi < i);
-            d = take ? od : d;
-            i = take ? oi : i;
-            w = take ? ow : w;
-        }
-        if (lane == 0) { red_d[wave] = d; red_i[wave] = i; red_w[wave] = w; }
-        __syncthreads();
-        d = red_d[0];
-        i = red_i[0];
-        w = red_w[0];
-        for (int x = 1; x < 4; x++) {
-            if (red_d[x] < d || (red_d[x] == d && red_i[x] < i)) { d = red_d[x]; i = red_i[x]; w = red_w[x]; }
-        }
-        __syncthreads();
-    };
-    int produced = 0, pos_old = 0;   // block-uniform
-    double fd = -1.0;                // floor key (fd, fi): smaller keys are taken
-    int fi = -1;
+    // running list of each query: old (read) and new (written at the end)
+    double nd[QW][NS];
+    int ni[QW][NS];
+    int produced[QW], pos_old[QW];
+    double fd[QW];
+    int fi[QW];
+#pragma unroll
+    for (int x = 0; x < QW; x++) {
+#pragma unroll
+        for (int s = 0; s < NS; s++) { nd[x][s] = KNN_INF; ni[x][s] = -1; }
+        produced[x] = 0;
+        pos_old[x] = 0;
+        fd[x] = -1.0;
+        fi[x] = -1;
+    }
+
     for (;;) {
-        double L[KT];
-        int I[KT];
+        double L[QW][KT];
+        int I[QW][KT], cnt[QW];
 #pragma unroll
-        for (int e = 0; e < KT; e++) { L[e] = KNN_INF; I[e] = 0x7fffffff; }
-        int cnt = 0;
-        for (int row = tid; row < nc; row += 256) {
-            const double S = knn_exact_sq<TE>(qa, cblk + (size_t)row * n_pad, n);
-            const double d = sqrt(S);
+        for (int x = 0; x < QW; x++) {
+            cnt[x] = 0;
+#pragma unroll
+            for (int e = 0; e < KT; e++) { L[x][e] = KNN_INF; I[x][e] = 0x7fffffff; }
+        }
+        for (int row = lane; row < nc; row += 64) {
+            const vec_t *cr = (const vec_t *)(cblk + (size_t)row * n_pad);
+            double S[QW] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 2
+            for (int p = 0; p < nr; p++) {
+                const vec_t c = cr[p];
+#pragma unroll
+                for (int x = 0; x < QW; x++) {
+                    const vec_t a = ((const vec_t *)qp[x])[p];
+#pragma unroll
+                    for (int e = 0; e < V; e++) {
+                        const double t = (double)a[e] - (double)c[e];
+                        const double t2 = t * t;
+                        S[x] = S[x] + t2;
+                    }
+                }
+            }
             const int id = (int)(c_base + row);
-            if (d != 0.0 && d < KNN_INF && (d > fd || (d == fd && id > fi))) {
-                cnt++;
-                list_insert<KT>(L, I, d, id);   // rows ascend: ties stay in id order
-            }
-        }
 #pragma unroll
-        for (int e = 0; e < KT; e++) {
-            sh_d[tid][e] = L[e];
-            sh_i[tid][e] = (L[e] == KNN_INF) ? 0x7fffffff : I[e];
-        }
-        double Bd = (cnt > KT) ? L[KT - 1] : KNN_INF;
-        int Bi = (cnt > KT) ? I[KT - 1] : 0x7fffffff, bw = 0;
-        block_min(Bd, Bi, bw);           // its barrier also publishes the lists
-        int pos = 0;
-        bool again = false;
-        while (produced < KP) {
-            double hd = (pos < KT) ? sh_d[tid][pos] : KNN_INF;
-            int hi = (pos < KT) ? sh_i[tid][pos] : 0x7fffffff, hw = tid;
-            if (tid == 0 && pos_old < KP) {
-                const double od = old_d[pos_old];
-                const int oi = old_i[pos_old];
-                if (od < hd || (od == hd && oi < hi)) { hd = od; hi = oi; hw = 256; }
+            for (int x = 0; x < QW; x++) {
+                const double d = sqrt(S[x]);
+                if (!done[x] && d != 0.0 && d < KNN_INF && d <= dcut[x] &&
+                    (d > fd[x] || (d == fd[x] && id > fi[x]))) {
+                    cnt[x]++;
+                    list_insert<KT>(L[x], I[x], d, id);   // rows ascend: ties stay in id order
+                }
             }
-            block_min(hd, hi, hw);
-            if (hd == KNN_INF) break;                                  // both sources empty
-            if (Bd < hd || (Bd == hd && Bi < hi)) { again = true; break; }  // past B
-            if (tid == 0) { new_d[produced] = hd; new_i[produced] = hi; }
-            produced++;
-            fd = hd;
-            fi = hi;
-            if (hw == 256) pos_old++;
-            else if (tid == hw) pos++;
         }
-        if (!again) break;
+        bool again_any = false;
+#pragma unroll
+        for (int x = 0; x < QW; x++) {
+            if (done[x]) continue;                        // wave-uniform
+            double Bd = (cnt[x] > KT) ? L[x][KT - 1] : KNN_INF;
+            int Bi = (cnt[x] > KT) ? I[x][KT - 1] : 0x7fffffff;
+            wave_argmin(Bd, Bi);
+            const double *od = rs_d + (size_t)slot[x] * KP;
+            const int *oi = rs_i + (size_t)slot[x] * KP;
+            int pos = 0;
+            bool again = false;
+            while (produced[x] < k) {
+                double hd = (pos < KT) ? L[x][0] : KNN_INF;
+                int hi = (pos < KT) ? I[x][0] : 0x7fffffff;
+                if (hd == KNN_INF) hi = 0x7fffffff;
+                bool mine = true;
+                if (lane == 0 && pos_old[x] < k) {
+                    const double v = od[pos_old[x]];
+                    const int vi = (v == KNN_INF) ? 0x7fffffff : oi[pos_old[x]];
+                    if (v < hd || (v == hd && vi < hi)) { hd = v; hi = vi; mine = false; }
+                }
+                double wd = hd;
+                int wi = hi;
+                wave_argmin(wd, wi);
+                if (wd == KNN_INF) break;                                  // both sources empty
+                if (Bd < wd || (Bd == wd && Bi < wi)) { again = true; break; }  // past B
+                const int r = produced[x];
+#pragma unroll
+                for (int s = 0; s < NS; s++)
+                    if (lane == (r & 63) && (r >> 6) == s) { nd[x][s] = wd; ni[x][s] = wi; }
+                produced[x]++;
+                fd[x] = wd;
+                fi[x] = wi;
+                const bool took = (hd == wd && hi == wi);
+                const unsigned long long who = __ballot(took);
+                const int wl = __builtin_ctzll(who);
+                const bool from_old = __shfl((int)(!mine), wl) != 0;
+                if (from_old) {
+                    pos_old[x]++;
+                } else if (lane == wl) {
+                    // pop the lane's head (lists are shifted so L[0] is the head)
+#pragma unroll
+                    for (int e = 0; e < KT - 1; e++) { L[x][e] = L[x][e + 1]; I[x][e] = I[x][e + 1]; }
+                    L[x][KT - 1] = KNN_INF;
+                    I[x][KT - 1] = 0x7fffffff;
+                    pos++;
+                }
+            }
+            if (!again) done[x] = true;
+            again_any |= again;
+        }
+        if (!again_any) break;
     }
-    __syncthreads();
-    for (int e = tid; e < KP; e += 256) {
-        rs_d[(size_t)slot * KP + e] = new_d[e];
-        rs_i[(size_t)slot * KP + e] = (new_d[e] == KNN_INF) ? -1 : new_i[e];
+    // all old-list reads precede the writes (the wave owns these slots)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int x = 0; x < QW; x++) {
+        if (slot[x] >= nfail) continue;
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            const int r = lane + 64 * s;
+            if (r < KP) {
+                rs_d[(size_t)slot[x] * KP + r] = nd[x][s];
+                rs_i[(size_t)slot[x] * KP + r] = (nd[x][s] == KNN_INF) ? -1 : ni[x][s];
+            }
+        }
     }
-    (void)q_base;
 }
 
 __global__ void k_fill_inf(double *p, int count)
@@ -1118,13 +1211,20 @@ template <typename T, int KL, int KP>
 static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int nq, const T *cblk,
                             size_t c_rows_pad, size_t c_base, int nc, int n, const double *meta,
                             int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
-                            double *qthr, hipStream_t s)
+                            double *qthr, int k, hipStream_t s)
 {
     constexpr int dt = sizeof(T) == 8 ? KNN_F64 : KNN_F32;
     const int np = (int)knn_n_pad_dt(n, dt);
     const int nqb = (nq + KNN_TQ - 1) / KNN_TQ;
     const int ntiles = (nc + KNN_TC - 1) / KNN_TC;
-    if (nqb <= 0 || nsplit <= 0) return KNN_ERR_INVALID;
+    if (nqb <= 0 || nsplit <= 0 || k <= 0 || k > KP) return KNN_ERR_INVALID;
+    // lane list slot of the shared bound (k_dist_topk): INT mode the max
+    // over lanes covers >= k+1 candidates, GEMM mode >= max(KP, k+1)
+    int uj_int = (k + 1 + 3) / 4 - 1;
+    if (uj_int > KL - 1) uj_int = KL - 1;
+    int uj_gemm = KP / 4 - 1 > uj_int ? KP / 4 - 1 : uj_int;
+    if (uj_gemm > KL - 1) uj_gemm = KL - 1;
+    const int uj = uj_int | (uj_gemm << 8);
     // geometry checks the kernel relies on (no out-of-bounds staging)
     if ((size_t)nqb * KNN_TQ > q_rows_pad || (size_t)ntiles * KNN_TC > c_rows_pad ||
         nq_pad < nqb * KNN_TQ)
@@ -1134,7 +1234,7 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP>), dim3((unsigned)(nqb * nsplit)),
                        dim3(512), 0, s, qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np,
                        ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                       (unsigned long long *)qthr);
+                       (unsigned long long *)qthr, uj);
     return hip_status();
 }
 
@@ -1147,7 +1247,7 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
         else return KNN_ERR_INVALID;                                           \
     } while (0)
 
-extern "C" int knn_launch_dist_topk(int dtype, int kp, const void *qblk, size_t q_rows_pad,
+extern "C" int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_rows_pad,
                                     size_t q_base, int nq, const void *cblk, size_t c_rows_pad,
                                     size_t c_base, int nc, int n, const double *meta, int nsplit,
                                     double *part_d, int *part_i, double *part_T, int nq_pad,
@@ -1156,7 +1256,7 @@ extern "C" int knn_launch_dist_topk(int dtype, int kp, const void *qblk, size_t 
 #define CALL(T, KL, KP)                                                                        \
     return launch_dist_topk<T, KL, KP>((const T *)qblk, q_rows_pad, q_base, nq, (const T *)cblk, \
                                        c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i,  \
-                                       part_T, nq_pad, qthr, (hipStream_t)stream)
+                                       part_T, nq_pad, qthr, k, (hipStream_t)stream)
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
 }
@@ -1184,7 +1284,7 @@ extern "C" int knn_launch_finalize(int dtype, int kp, const double *st_d, const 
                                    const int *st_i, const double *st_T, const void *qblk,
                                    size_t q_rows_pad, int nq, int n, int k, const double *meta,
                                    knn_neighbour_t *out, int *fail_count, int *fail_list,
-                                   int *mode_out, void *stream)
+                                   int *mode_out, double *fbound, void *stream)
 {
     if (k <= 0 || k > kp) return KNN_ERR_INVALID;
     const size_t off = q_rows_pad * knn_n_pad_dt(n, dtype);
@@ -1193,7 +1293,7 @@ extern "C" int knn_launch_finalize(int dtype, int kp, const double *st_d, const 
 #define CALL(T, KL, KP)                                                                        \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_finalize<T, KP>), grid, dim3(256), 0, s, st_d, st_x,   \
                        st_i, st_T, (const T *)qblk + off, nq, n, k, meta, out, fail_count,       \
-                       fail_list, mode_out);                                                     \
+                       fail_list, mode_out, fbound);                                             \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
@@ -1209,17 +1309,18 @@ extern "C" int knn_launch_rescan_init(int kp, double *rs_d, int *rs_i, int nfail
 }
 
 extern "C" int knn_launch_rescan_step(int dtype, int kp, const int *fail_list, int nfail,
-                                      const void *qblk, size_t q_base, const void *cblk,
-                                      size_t c_base, int nc, int n, double *rs_d, int *rs_i,
-                                      void *stream)
+                                      const double *fbound, const void *qblk, const void *cblk,
+                                      size_t c_base, int nc, int n, int k, double *rs_d,
+                                      int *rs_i, void *stream)
 {
     if (nfail <= 0) return KNN_OK;
+    if (k <= 0 || k > kp) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
     hipStream_t s = (hipStream_t)stream;
-#define CALL(T, KL, KP)                                                                         \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_step<T, KP>), dim3((unsigned)nfail), dim3(256), 0, \
-                       s, fail_list, (const T *)qblk, np, q_base, (const T *)cblk, c_base, nc, n,  \
-                       np, rs_d, rs_i);                                                           \
+#define CALL(T, KL, KP)                                                                          \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_step<T, KP>), dim3((unsigned)((nfail + 15) / 16)), \
+                       dim3(256), 0, s, fail_list, nfail, fbound, (const T *)qblk, np,            \
+                       (const T *)cblk, c_base, nc, n, np, k, rs_d, rs_i);                        \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL

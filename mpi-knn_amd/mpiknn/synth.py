@@ -26,3 +26,38 @@ def mnist_like(m=60000, n=784, seed=1234):
     np.rint(X, out=X)
     np.clip(X, 0, 255, out=X)
     return X, (y + 1).astype(np.float64)
+
+
+def sift_like(m=1_000_000, n=128, clusters=1024, seed=0x51F7, chunk=1 << 18):
+    """BASELINE.json configs[3] shape: SIFT-like 1M x 128, a mixture of
+    `clusters` Gaussian centres clipped to [0, 255] and rounded (integer
+    valued like SIFT descriptors), returned as float32 row-major (the fvecs
+    layout).  Generated in chunks so 1M+ rows stay cheap."""
+    rng = np.random.default_rng(seed)
+    centres = rng.uniform(0, 160, (clusters, n)).astype(np.float32)
+    X = np.empty((m, n), dtype=np.float32)
+    for lo in range(0, m, chunk):
+        hi = min(m, lo + chunk)
+        lab = rng.integers(0, clusters, hi - lo)
+        blk = centres[lab] + rng.normal(0, 25, (hi - lo, n)).astype(np.float32)
+        np.rint(blk, out=blk)
+        np.clip(blk, 0, 255, out=blk)
+        X[lo:hi] = blk
+    return X
+
+
+def gist_like(m=4_000_000, n=960, clusters=256, seed=0x6157, chunk=1 << 16):
+    """BASELINE.json configs[4] shape: GIST-like x 960 real-valued features
+    in [0, 1) (mixture of `clusters` centres + N(0, 0.08)), float32
+    row-major."""
+    rng = np.random.default_rng(seed)
+    centres = rng.uniform(0.1, 0.6, (clusters, n)).astype(np.float32)
+    X = np.empty((m, n), dtype=np.float32)
+    top = np.nextafter(np.float32(1), np.float32(0))
+    for lo in range(0, m, chunk):
+        hi = min(m, lo + chunk)
+        lab = rng.integers(0, clusters, hi - lo)
+        blk = centres[lab] + rng.normal(0, 0.08, (hi - lo, n)).astype(np.float32)
+        np.clip(blk, 0, top, out=blk)
+        X[lo:hi] = blk
+    return X
