@@ -207,7 +207,12 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     c->n = n;
     c->block_cap = block_cap;
     c->k = k;
-    c->kp = knn_kp_for(k);
+    c->kp = knn_kp_for(k, dtype);
+    /* tuning override: an fp32 context may take any variant holding k */
+    if (dtype == KNN_F32 && getenv("KNN_FORCE_KP")) {
+        const int f = atoi(getenv("KNN_FORCE_KP"));
+        if ((f == KNN_KP || f == KNN_KP_M || f == KNN_KP_L) && k <= f) c->kp = f;
+    }
     c->kl = knn_kl_for(c->kp);
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
 
@@ -344,9 +349,9 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
                               c->part_d, c->part_i, c->part_T, (int)c->nq_pad, c->qthr, stream));
     if (ev) HIPCHK(hipEventRecord(ev[1], (hipStream_t)stream));
-    RCHK(knn_launch_merge(c->dtype, c->kp, c->part_d, c->part_i, c->part_T, nsplit, (int)c->nq, (int)c->nq_pad,
-                          c->first_step, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, cblk,
-                          c_base, (int)nc, (int)c->n, c->meta, stream));
+    RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d, c->part_i, c->part_T, nsplit, (int)c->nq,
+                          (int)c->nq_pad, c->first_step, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk,
+                          c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n, c->meta, stream));
     if (ev) HIPCHK(hipEventRecord(ev[2], (hipStream_t)stream));
     c->first_step = 0;
     return KNN_OK;

@@ -18,7 +18,9 @@ extern "C" {
 #define KNN_BK 16         /* fp64 features per LDS chunk (128 B a row) */
 #define KNN_KL 16         /* per-lane candidate list capacity, k <= 32 */
 #define KNN_KP 32         /* per-query state / selection capacity      */
-#define KNN_KL_L 40       /* the same for 32 < k <= 128 (fp32 only):   */
+#define KNN_KL_M 24       /* fp32, 16 < k <= 32: a lane list overflows */
+#define KNN_KP_M 64       /*   when > KL of the k fall in its quarter   */
+#define KNN_KL_L 40       /* fp32, 32 < k <= 128:                        */
 #define KNN_KP_L 128      /*   P(Bin(100, 1/4) > 40) ~ 3e-4 per lane   */
 #define KNN_ROW_ALIGN 128 /* packed-block row padding                  */
 
@@ -41,8 +43,18 @@ static inline size_t knn_n_pad(size_t n) { return knn_round_up(n ? n : 1, KNN_BK
 /* element size and padded row length of a packed block of `dtype`
  * (KNN_F64 / KNN_F32): rows are padded to whole 128-byte chunks */
 /* state capacity and per-lane list length serving k */
-static inline int knn_kp_for(int k) { return k <= KNN_KP ? KNN_KP : KNN_KP_L; }
-static inline int knn_kl_for(int kp) { return kp == KNN_KP ? KNN_KL : KNN_KL_L; }
+/* State capacity serving k.  With one corpus split, 16-deep lane lists
+ * overflow for P(Bin(32, 1/4) >= 16) * 4 = 0.8% of queries at k = 32 (each
+ * a rescan); fp32 has the registers for deeper lists, fp64 (k <= 32) not. */
+static inline int knn_kp_for(int k, int dtype)
+{
+    if (dtype != KNN_F32 || k <= 16) return KNN_KP;
+    return k <= 32 ? KNN_KP_M : KNN_KP_L;
+}
+static inline int knn_kl_for(int kp)
+{
+    return kp == KNN_KP ? KNN_KL : kp == KNN_KP_M ? KNN_KL_M : KNN_KL_L;
+}
 static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
 {
@@ -59,11 +71,11 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
                          double *part_d, int *part_i, double *part_T, int nq_pad,
                          double *qthr, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
-int knn_launch_merge(int dtype, int kp, const double *part_d, const int *part_i, const double *part_T,
-                     int nsplit, int nq, int nq_pad, int first_step,
-                     double *st_d, double *st_x, int *st_i, double *st_T,
-                     const void *qblk, const void *cblk, size_t c_base, int nc,
-                     int n, const double *meta, void *stream);
+int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *part_i,
+                     const double *part_T, int nsplit, int nq, int nq_pad, int first_step,
+                     double *st_d, double *st_x, int *st_i, double *st_T, const void *qblk,
+                     size_t q_rows_pad, const void *cblk, size_t c_base, int nc, int n,
+                     const double *meta, void *stream);
 int knn_launch_finalize(int dtype, int kp, const double *st_d, const double *st_x, const int *st_i,
                         const double *st_T, const void *qblk, size_t q_rows_pad,
                         int nq, int n, int k, const double *meta,

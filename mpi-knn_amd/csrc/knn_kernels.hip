@@ -97,18 +97,45 @@ __device__ __forceinline__ int knn_mode(const double *meta, int n)
 // Reference-order exact squared distance: S = S + (a-b)^2 over j = 0..n-1,
 // two roundings per feature, no FMA (knn-serial.c:76-85; pow(x,2) -> x*x),
 // in fp64 on the block's values (fp32 blocks: the fp32-rounded inputs).
+// Read 16 bytes at a time: rows are zero padded to n_pad (a multiple of 16
+// bytes) and S + (0-0)^2 = S, so running the loop to a whole 16 B leaves S
+// bit-identical.
 template <typename T>
-__device__ __attribute__((noinline)) double knn_exact_sq(const T *__restrict__ a,
-                                                         const T *__restrict__ b, int n)
+__device__ __forceinline__ double knn_exact_sq_v(const T *__restrict__ a, const T *__restrict__ b,
+                                                 int n)
 {
 #pragma clang fp contract(off)
+    typedef typename std::conditional<sizeof(T) == 8, dbl2, flt4>::type vec_t;
+    constexpr int V = 16 / (int)sizeof(T);
+    const int nr = (n + V - 1) / V;
     double S = 0.0;
-    for (int j = 0; j < n; j++) {
-        double t = (double)a[j] - (double)b[j];
-        double t2 = t * t;
-        S = S + t2;
+#pragma unroll 2
+    for (int p = 0; p < nr; p++) {
+        const vec_t va = ((const vec_t *)a)[p];
+        const vec_t vb = ((const vec_t *)b)[p];
+#pragma unroll
+        for (int e = 0; e < V; e++) {
+            const double t = (double)va[e] - (double)vb[e];
+            const double t2 = t * t;
+            S = S + t2;
+        }
     }
     return S;
+}
+
+// Certificate margin: |GEMM-form d^2 - exact S| plus the reference's own
+// rounding, for any candidate c of the search (|c|^2 <= maxnorm):
+//   fp32 filter: fma-chain dot gamma_n (|q|^2+|c|^2), norm roundings and the
+//   two final roundings 4u (|q|^2+|c|^2), times (1 + 2(n+4)u) for the
+//   second-order terms; the reference's fp64 S: 4(n+2) 2^-53 (|q|^2+|c|^2).
+//   fp64 filter: both at u = 2^-53, 8(n+4)u (|q|^2+|c|^2).
+template <typename TE>
+__device__ __forceinline__ double knn_cert_E(int n, double qn, double maxnorm)
+{
+    const double u = KT<TE>::U;
+    const double nn = (double)n + 4.0, qc = qn + maxnorm;
+    if constexpr (sizeof(TE) == 8) return 8.0 * nn * u * qc;
+    else return nn * qc * (u * (1.0 + 2.0 * nn * u) + 4.0 * 1.1102230246251565e-16);
 }
 
 // ---------------------------------------------------------------------------
@@ -683,9 +710,9 @@ __global__ __launch_bounds__(256) void k_merge(
     const double *__restrict__ part_d, const int *__restrict__ part_i,
     const double *__restrict__ part_T, int nsplit, int nq, int nq_pad, int first_step,
     double *__restrict__ st_d, double *__restrict__ st_x, int *__restrict__ st_i,
-    double *__restrict__ st_T, const TE *__restrict__ qblk,
+    double *__restrict__ st_T, const TE *__restrict__ qblk, size_t qnorm_off,
     const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
-    const double *__restrict__ meta)
+    const double *__restrict__ meta, int k)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + wave;
@@ -760,6 +787,29 @@ __global__ __launch_bounds__(256) void k_merge(
         }
     }
 
+    // GEMM mode: exact S of the new entries, from the resident block.  Let
+    // z = the entries with d^2 <= E (possibly S == 0: excluded results) and
+    // d^2_k the (k+z)-th d^2 of the new state.  An entry with d^2 > d^2_k +
+    // 2E has S > d^2_k + E >= the k-th smallest nonzero S of the state, now
+    // and after any later merge (d^2_k only falls), so it can never reach
+    // the top k: its S is skipped and marked +inf (k_finalize ignores it).
+    double win = KNN_INF;
+    if (mode == KNN_MODE_GEMM) {
+        const double E = knn_cert_E<TE>(n, (double)qblk[qnorm_off + q], meta[KNN_META_MAXNORM]);
+        int z = 0;
+#pragma unroll
+        for (int x = 0; x < NS; x++) z += __popcll(__ballot(lane + 64 * x < KP && sd[x] <= E));
+        const int rk = k - 1 + z;
+        double dk = KNN_INF;
+        if (rk < KP) {
+#pragma unroll
+            for (int x = 0; x < NS; x++) {
+                const double v = __shfl(sd[x], rk & 63);
+                if ((rk >> 6) == x) dk = v;
+            }
+        }
+        if (dk < KNN_INF) win = (dk + 2.0 * E) * (1.0 + 1.0 / 1048576.0);
+    }
     double sx[NS];
 #pragma unroll
     for (int x = 0; x < NS; x++) {
@@ -767,9 +817,11 @@ __global__ __launch_bounds__(256) void k_merge(
         if (lane + 64 * x < KP && mode == KNN_MODE_GEMM && si[x] >= 0) {
             if (ssrc[x]) {
                 sx[x] = st_x[(size_t)q * KP + spos[x]];
-            } else {
+            } else if (sd[x] <= win) {
                 const int row = (int)((long)si[x] - (long)c_base);
-                sx[x] = knn_exact_sq<TE>(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n);
+                sx[x] = knn_exact_sq_v<TE>(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n);
+            } else {
+                sx[x] = KNN_INF;
             }
         }
     }
@@ -916,17 +968,9 @@ __global__ __launch_bounds__(256) void k_finalize(
             const unsigned long long at = __ballot(valid[x] && rank[x] == kl);
             if (at) tau = __shfl(sx[x], __builtin_ctzll(at));
         }
-        // E bounds |GEMM-form d^2 - exact S| plus the reference's own
-        // rounding, for any candidate c (|c|^2 <= maxnorm):
-        //   fp32 filter: fma-chain dot  gamma_n (|q|^2+|c|^2), norm
-        //   roundings and the two final roundings 4u (|q|^2+|c|^2), times
-        //   (1 + 2(n+4)u) for the second-order terms; the reference's fp64
-        //   S: 4(n+2) 2^-53 (|q|^2+|c|^2).
-        //   fp64 filter: both at u = 2^-53, 8(n+4)u (|q|^2+|c|^2).
-        const double u = KT<TE>::U;
-        const double nn = (double)n + 4.0, qc = (double)qnorm[q] + meta[KNN_META_MAXNORM];
-        const double E = (sizeof(TE) == 8) ? 8.0 * nn * u * qc
-                                           : nn * qc * (u * (1.0 + 2.0 * nn * u) + 4.0 * 1.1102230246251565e-16);
+        // E (knn_cert_E): |GEMM-form d^2 - exact S| plus the reference's
+        // own rounding; T and Td are GEMM-form values
+        const double E = knn_cert_E<TE>(n, (double)qnorm[q], meta[KNN_META_MAXNORM]);
         ok = (Tb == KNN_INF) || ((Tb - E) > tau * (1.0 + 1.7763568394002505e-15));
     } else {
         ok = (Tb == KNN_INF);
@@ -1238,11 +1282,12 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     return hip_status();
 }
 
-// The served (element type, state capacity) pairs: fp64 k <= 32, fp32 k <= 128.
+// The served (element type, state capacity) pairs: fp64 k <= 32; fp32 k <= 16, 32, 128.
 #define KNN_DISPATCH(dtype, kp, CALL)                                          \
     do {                                                                       \
         if ((dtype) == KNN_F64 && (kp) == KNN_KP) { CALL(double, KNN_KL, KNN_KP); }       \
         else if ((dtype) == KNN_F32 && (kp) == KNN_KP) { CALL(float, KNN_KL, KNN_KP); }   \
+        else if ((dtype) == KNN_F32 && (kp) == KNN_KP_M) { CALL(float, KNN_KL_M, KNN_KP_M); } \
         else if ((dtype) == KNN_F32 && (kp) == KNN_KP_L) { CALL(float, KNN_KL_L, KNN_KP_L); } \
         else return KNN_ERR_INVALID;                                           \
     } while (0)
@@ -1261,20 +1306,22 @@ extern "C" int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, 
 #undef CALL
 }
 
-extern "C" int knn_launch_merge(int dtype, int kp, const double *part_d, const int *part_i,
+extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *part_i,
                                 const double *part_T, int nsplit, int nq, int nq_pad,
                                 int first_step, double *st_d, double *st_x, int *st_i,
-                                double *st_T, const void *qblk, const void *cblk, size_t c_base,
-                                int nc, int n, const double *meta, void *stream)
+                                double *st_T, const void *qblk, size_t q_rows_pad,
+                                const void *cblk, size_t c_base, int nc, int n,
+                                const double *meta, void *stream)
 {
-    if (4 * nsplit + 1 > 64) return KNN_ERR_INVALID;
+    if (4 * nsplit + 1 > 64 || k <= 0 || k > kp) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
+    const size_t qn_off = q_rows_pad * (size_t)np;
     const dim3 grid((unsigned)((nq + 3) / 4));
     hipStream_t s = (hipStream_t)stream;
 #define CALL(T, KL, KP)                                                                         \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KL, KP>), grid, dim3(256), 0, s, part_d, part_i, \
                        part_T, nsplit, nq, nq_pad, first_step, st_d, st_x, st_i, st_T,            \
-                       (const T *)qblk, (const T *)cblk, c_base, nc, n, np, meta);               \
+                       (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n, np, meta, k);    \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
