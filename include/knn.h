@@ -124,6 +124,19 @@ KNN_API double knn_last_search_seconds(void);
 KNN_API int knn_classify(const knn_neighbour_t *nb, size_t m, int k, int nclasses,
                  int vote_rule, const double *labels, int *pred, size_t *matches);
 
+/* The same vote on the device, on the records knn_ctx_end / rescan_end
+ * wrote (no host round trip).  d_nb: m*k records of queries with global ids
+ * q_base..q_base+m-1, whose .label it fills (blk:176); d_labels: nlabels
+ * row labels (global id i at d_labels[i-1]; ids > nlabels count as empty);
+ * d_pred (nullable): m predictions; d_matches (nullable): one device
+ * counter, set to the number of queries predicted as their own label.
+ * nclasses <= KNN_VOTE_MAX_CLASSES (else KNN_ERR_UNSUPPORTED: use the host
+ * knn_classify). */
+#define KNN_VOTE_MAX_CLASSES 1024
+KNN_API int knn_classify_device(knn_neighbour_t *d_nb, size_t m, int k, int nclasses,
+                        int vote_rule, const double *d_labels, size_t nlabels, size_t q_base,
+                        int *d_pred, unsigned long long *d_matches, void *stream);
+
 /* ---------------------------------------------------------------------- *
  * Device-resident API (the engine underneath knn_search; used by the
  * per-rank RCCL ring driver and by bench.py).  All pointers named d_* are

@@ -88,6 +88,9 @@ int knn_launch_rescan_step(int dtype, int kp, const int *fail_list, int nfail,
                            void *stream);
 int knn_launch_rescan_end(int kp, const int *fail_list, int nfail, const double *rs_d,
                           const int *rs_i, int k, knn_neighbour_t *out, void *stream);
+int knn_launch_vote(knn_neighbour_t *nb, size_t m, int k, int nclasses, int rule,
+                    const double *labels, size_t nlabels, size_t q_base, int *pred,
+                    unsigned long long *matches, void *stream);
 
 #ifdef __cplusplus
 }

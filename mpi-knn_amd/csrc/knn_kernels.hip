@@ -1382,3 +1382,91 @@ extern "C" int knn_launch_rescan_end(int kp, const int *fail_list, int nfail, co
                        (hipStream_t)stream, fail_list, nfail, kp, rs_d, rs_i, k, out);
     return hip_status();
 }
+
+// ---------------------------------------------------------------------------
+// k_vote: the label vote + accuracy stage on the device (knn_classify_device;
+// host twin knn_vote.c, same rules).  One wave per query: the k neighbour
+// labels are counted into the wave's LDS histogram (nclasses <= 1024), lane
+// 0 walks the classes in label order exactly like serial:121-124 /
+// blk:263-266 (SERIAL / MPI, with their count-vs-label quirk) or
+// takes a true majority (MAJORITY), then compares with the query's own
+// label (serial:126-127).  The neighbour records get their .label filled
+// (blk:176).  Empty slots and idx > nlabels are skipped.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_vote(knn_neighbour_t *__restrict__ nb, int m, int k,
+                                              int nclasses, int rule,
+                                              const double *__restrict__ labels,
+                                              long long nlabels, long long q_base,
+                                              int *__restrict__ pred,
+                                              unsigned long long *__restrict__ matches)
+{
+    __shared__ int cls[4][KNN_VOTE_MAX_CLASSES];
+    __shared__ unsigned hits[4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + wave;
+    int *c = cls[wave];
+    for (int j = lane; j < nclasses; j += 64) c[j] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    unsigned hit = 0;
+    if (q < m) {
+        knn_neighbour_t *L = nb + (size_t)q * k;
+        for (int i = lane; i < k; i += 64) {
+            const int id = L[i].idx;
+            int lab = 0;
+            if (id > 0 && id <= nlabels) {
+                lab = (int)labels[id - 1];
+                L[i].label = lab;
+                if (lab >= 1 && lab <= nclasses) atomicAdd(&c[lab - 1], 1);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane == 0) {
+            int most = 0;
+            if (rule == KNN_VOTE_MAJORITY) {
+                int best = 0;
+                for (int j = 0; j < nclasses; j++) best = c[j] > best ? c[j] : best;
+                for (int i = 0; i < k && best > 0; i++) {
+                    const int id = L[i].idx;
+                    if (id <= 0 || id > nlabels) continue;
+                    const int lab = (int)labels[id - 1];
+                    if (lab >= 1 && lab <= nclasses && c[lab - 1] == best) {
+                        most = lab;
+                        break;
+                    }
+                }
+            } else {
+                const int id0 = L[0].idx;
+                const int nn0 = (id0 > 0 && id0 <= nlabels) ? (int)labels[id0 - 1] : 0;
+                const int tie = rule == KNN_VOTE_MPI ? nn0 - 1 : nn0;
+                for (int j = 0; j < nclasses; j++)
+                    if (c[j] > most || (c[j] == most && (j + 1) == tie)) most = j + 1;
+            }
+            if (pred) pred[q] = most;
+            const long long g = q_base + q;
+            hit = (g < nlabels && (double)most == labels[g]) ? 1u : 0u;
+        }
+    }
+    if (lane == 0) hits[wave] = hit;
+    __syncthreads();
+    if (threadIdx.x == 0 && matches) {
+        const unsigned h = hits[0] + hits[1] + hits[2] + hits[3];
+        if (h) atomicAdd(matches, (unsigned long long)h);
+    }
+}
+
+extern "C" int knn_launch_vote(knn_neighbour_t *nb, size_t m, int k, int nclasses, int rule,
+                               const double *labels, size_t nlabels, size_t q_base, int *pred,
+                               unsigned long long *matches, void *stream)
+{
+    if (m == 0) return KNN_OK;
+    if (nclasses > KNN_VOTE_MAX_CLASSES || m > 0x7fffffffULL) return KNN_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    if (matches && hipMemsetAsync(matches, 0, sizeof(unsigned long long), s) != hipSuccess)
+        return KNN_ERR_HIP;
+    hipLaunchKernelGGL(k_vote, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, s, nb, (int)m, k,
+                       nclasses, rule, labels, (long long)nlabels, (long long)q_base, pred, matches);
+    return hip_status();
+}

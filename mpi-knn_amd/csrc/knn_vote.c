@@ -10,7 +10,9 @@
  * search, and the reference excludes it from its timer (serial:94-98).
  */
 #include "knn.h"
+#include "knn_internal.h"
 
+#include <hip/hip_runtime_api.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -57,4 +59,19 @@ int knn_classify(const knn_neighbour_t *nb, size_t m, int k, int nclasses, int v
     free(cls);
     if (matches) *matches = hit;
     return KNN_OK;
+}
+
+/* The same stage on device-resident records (k_vote in knn_kernels.hip):
+ * one wave per query, no host round trip between search and vote. */
+int knn_classify_device(knn_neighbour_t *d_nb, size_t m, int k, int nclasses, int vote_rule,
+                        const double *d_labels, size_t nlabels, size_t q_base, int *d_pred,
+                        unsigned long long *d_matches, void *stream)
+{
+    if (!d_nb || !d_labels || k <= 0 || nclasses <= 0) return KNN_ERR_INVALID;
+    if (vote_rule != KNN_VOTE_SERIAL && vote_rule != KNN_VOTE_MPI &&
+        vote_rule != KNN_VOTE_MAJORITY)
+        return KNN_ERR_INVALID;
+    if (nclasses > KNN_VOTE_MAX_CLASSES) return KNN_ERR_UNSUPPORTED;
+    return knn_launch_vote(d_nb, m, k, nclasses, vote_rule, d_labels, nlabels, q_base, d_pred,
+                           d_matches, stream);
 }

@@ -40,7 +40,7 @@ API_SYMBOLS = (
     "knn_ctx_create", "knn_ctx_destroy", "knn_ctx_begin", "knn_ctx_step", "knn_ctx_end",
     "knn_ctx_rescan_step", "knn_ctx_rescan_end", "knn_search_packed", "knn_ctx_info",
     "knn_ctx_profile", "knn_block_bytes_dt", "knn_block_meta_offset_dt", "knn_block_pack_dt",
-    "knn_ctx_create_dt",
+    "knn_ctx_create_dt", "knn_classify_device",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -89,6 +89,7 @@ def _load():
         "knn_block_pack_dt": ([p, i, sz, sz, sz, p, i, sz, i, p], i),
         "knn_ctx_create_dt": ([pp, i, sz, sz, sz, i, i], i),
         "knn_ctx_destroy": ([p], i),
+        "knn_classify_device": ([p, sz, i, i, i, p, sz, sz, p, p, p], i),
         "knn_ctx_begin": ([p, p, sz, sz, p, p], i),
         "knn_ctx_step": ([p, p, sz, sz, p], i),
         "knn_ctx_end": ([p, p, psz, p], i),
@@ -182,6 +183,18 @@ def classify(nb, labels, nclasses=10, rule=VOTE_SERIAL):
 
 
 # ------------------------------------------------------ device-resident API
+
+VOTE_MAX_CLASSES = 1024
+
+
+def classify_device(d_nb, m, k, nclasses, rule, d_labels, nlabels, q_base=0, d_pred=None,
+                    d_matches=None, stream=0):
+    """knn_classify_device on device pointers (ints): fills the records'
+    labels, writes m predictions to d_pred and the match count (uint64) to
+    d_matches (both nullable)."""
+    _check(lib.knn_classify_device(d_nb, m, k, nclasses, rule, d_labels, nlabels, q_base,
+                                   d_pred or None, d_matches or None, stream or None),
+           "knn_classify_device")
 
 def block_bytes(cap, n, dtype="f64"):
     return lib.knn_block_bytes_dt(cap, n, DTYPES[dtype])

@@ -58,6 +58,11 @@ def test_invalid_arguments(knn):
         == knn.ERR_INVALID
     assert lib.knn_ctx_create_dt(ctypes.byref(h), 0, 4, 2, 4, 129, 1) == knn.ERR_INVALID
     assert knn.MAX_K == 32 and knn.MAX_K_F32 == 128
+    q = ctypes.c_void_p(8)   # never dereferenced: argument checks come first
+    assert lib.knn_classify_device(None, 4, 3, 10, 0, q, 4, 0, None, None, None) == knn.ERR_INVALID
+    assert lib.knn_classify_device(q, 4, 3, 10, 9, q, 4, 0, None, None, None) == knn.ERR_INVALID
+    assert lib.knn_classify_device(q, 4, 3, 2000, 0, q, 4, 0, None, None, None) == \
+        knn.ERR_UNSUPPORTED
     assert lib.knn_search(p, 4, 2, 1, None, 3, 0, 0, o) == knn.ERR_INVALID
     h = ctypes.c_void_p()
     assert lib.knn_ctx_create(ctypes.byref(h), 0, 0, 2, 4, 3) == knn.ERR_INVALID

@@ -116,11 +116,18 @@ def test_f32_nonfinite_scan(knn, oracle):
 
 
 @pytest.mark.parametrize("what,k", [("gist_like", 100), ("sift_like", 64), ("gaussian", 128),
-                                    ("gist_like", 31), ("mnist_like", 100), ("binary", 100)])
+                                    ("gist_like", 31), ("mnist_like", 100), ("binary", 100),
+                                    ("gaussian", 16), ("gaussian", 17), ("gaussian", 33),
+                                    ("dups", 17), ("dups", 100), ("sift_like", 32)])
 def test_f32_large_k(knn, oracle, what, k):
-    """k > 32 (BASELINE configs[4]: k = 100) -- the 128-slot state and the
-    40-deep per-lane lists; every engine mode."""
-    if what == "gist_like":
+    """k > 16: the 64-slot (24-deep lane lists, k <= 32) and 128-slot
+    (40-deep, k <= 128; BASELINE configs[4]: k = 100) states at their
+    boundaries, in every engine mode; exact duplicates (S == 0 entries next
+    to the merge's exact-S window)."""
+    if what == "dups":
+        X, _ = datasets.digits()
+        X = np.vstack([X, X[:40], X[:40]]) / 3.0
+    elif what == "gist_like":
         X = datasets.gist_like(1500, 960, clusters=24, seed=k)
     elif what == "sift_like":
         X = datasets.sift_like(2500, 128, clusters=32, seed=7)   # fp32 INT mode

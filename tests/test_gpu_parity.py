@@ -68,6 +68,17 @@ def test_gaussian_real(knn, oracle, m, n):
     assert_same(got, ref, "gaussian %dx%d" % (m, n))
 
 
+@pytest.mark.parametrize("k", [1, 2, 31, 32])
+def test_k_range_fp64(knn, oracle, k):
+    """k from 1 to KNN_MAX_K in both exact modes, with duplicate rows (S == 0
+    entries beside the merge's exact-S window) in the real-valued case."""
+    X, _ = datasets.digits()
+    X = np.vstack([X, X[:30], X[:30]])
+    assert_same(knn.search(X, k)[0], oracle.knn(X, k), "digits+dups k=%d" % k)
+    Xr = X / 7.0 + 0.001
+    assert_same(knn.search(Xr, k)[0], oracle.knn(Xr, k), "real+dups k=%d" % k)
+
+
 def test_fewer_rows_than_k(knn, oracle):
     X = np.arange(40, dtype=np.float64).reshape(10, 4)
     ref = oracle.knn(X, 30)
