@@ -34,6 +34,7 @@ struct knn_ctx {
     size_t nq, nq_pad, n, block_cap;
     int k;
     int kp, kl;         /* state capacity / per-lane list length serving k */
+    int xord;           /* k_dist_topk workgroup order (0 split-major, 1 XCD-grouped) */
     int cus;
     /* per-step partial lists of k_dist_topk, grown to the largest split
      * count used so far (part_splits) */
@@ -214,6 +215,7 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
         if ((f == KNN_KP || f == KNN_KP_M || f == KNN_KP_L) && k <= f) c->kp = f;
     }
     c->kl = knn_kl_for(c->kp);
+    c->xord = getenv("KNN_XCD_ORDER") ? atoi(getenv("KNN_XCD_ORDER")) != 0 : 0;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
 
     const size_t np = c->nq_pad;
@@ -347,7 +349,8 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     }
     RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
-                              c->part_d, c->part_i, c->part_T, (int)c->nq_pad, c->qthr, stream));
+                              c->part_d, c->part_i, c->part_T, (int)c->nq_pad, c->qthr, c->xord,
+                              stream));
     if (ev) HIPCHK(hipEventRecord(ev[1], (hipStream_t)stream));
     RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d, c->part_i, c->part_T, nsplit, (int)c->nq,
                           (int)c->nq_pad, c->first_step, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk,

@@ -362,7 +362,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const T *__restrict__ cblk, const T *__restrict__ cnorm, size_t c_base, int nc,
     int n, int n_pad, int ntiles, int nsplit, int nqb, const double *__restrict__ meta,
     double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T,
-    int nq_pad, unsigned long long *__restrict__ qthr, int uj)
+    int nq_pad, unsigned long long *__restrict__ qthr, int uj, int xord)
 {
     constexpr int NST = KNN_NST;
     constexpr int BK = knn_bk<T>();                   // features per 128-B chunk
@@ -373,9 +373,23 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     __shared__ __attribute__((aligned(16))) char smem[NST * 32768 + 8192];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane >> 4, j16 = lane & 15;
-    // split-major order: the first resident wave of workgroups shares one
-    // corpus split, so its tiles are read from L2 by every XCD's workgroups
-    const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;
+    // xord 0, split-major: the first resident wave of workgroups shares one
+    // corpus split, so its tiles are read from L2 by every XCD's workgroups.
+    // xord 1, XCD-grouped: workgroups go to XCDs round-robin (blockIdx % 8),
+    // so the nsplit workgroups of query block qb get ids 8(j nsplit + s) +
+    // (qb % 8): one XCD, dispatched back to back -- they stream the same
+    // query chunks in step (L2 hits), and co-resident blocks of one split
+    // share corpus tiles.  The grid is padded to whole groups of 8 blocks.
+    int qb, split;
+    if (xord) {
+        const int slot = blockIdx.x >> 3;
+        split = slot % nsplit;
+        qb = ((slot / nsplit) << 3) + (blockIdx.x & 7);
+        if (qb >= nqb) return;
+    } else {
+        qb = blockIdx.x % nqb;
+        split = blockIdx.x / nqb;
+    }
     const int t_lo = (int)((long)split * ntiles / nsplit);
     const int t_hi = (int)((long)(split + 1) * ntiles / nsplit);
     const int mode = knn_mode<T>(meta, n);
@@ -1255,7 +1269,7 @@ template <typename T, int KL, int KP>
 static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int nq, const T *cblk,
                             size_t c_rows_pad, size_t c_base, int nc, int n, const double *meta,
                             int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
-                            double *qthr, int k, hipStream_t s)
+                            double *qthr, int k, int xord, hipStream_t s)
 {
     constexpr int dt = sizeof(T) == 8 ? KNN_F64 : KNN_F32;
     const int np = (int)knn_n_pad_dt(n, dt);
@@ -1275,10 +1289,11 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
         return KNN_ERR_INVALID;
     const T *qnorm = qblk + q_rows_pad * np;
     const T *cnorm = cblk + c_rows_pad * np;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP>), dim3((unsigned)(nqb * nsplit)),
+    const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP>), dim3((unsigned)(nqb_grid * nsplit)),
                        dim3(512), 0, s, qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np,
                        ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                       (unsigned long long *)qthr, uj);
+                       (unsigned long long *)qthr, uj, xord);
     return hip_status();
 }
 
@@ -1296,12 +1311,12 @@ extern "C" int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, 
                                     size_t q_base, int nq, const void *cblk, size_t c_rows_pad,
                                     size_t c_base, int nc, int n, const double *meta, int nsplit,
                                     double *part_d, int *part_i, double *part_T, int nq_pad,
-                                    double *qthr, void *stream)
+                                    double *qthr, int xord, void *stream)
 {
 #define CALL(T, KL, KP)                                                                        \
     return launch_dist_topk<T, KL, KP>((const T *)qblk, q_rows_pad, q_base, nq, (const T *)cblk, \
                                        c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i,  \
-                                       part_T, nq_pad, qthr, k, (hipStream_t)stream)
+                                       part_T, nq_pad, qthr, k, xord, (hipStream_t)stream)
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
 }

@@ -46,13 +46,13 @@ float run(const double* blk, size_t rp, int m, int n, int nsplit, double* pd, in
     if (qthr) knn_launch_fill_inf(qthr, nq_pad, 0);
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<double, KNN_KL, KNN_KP, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
                        blk, norms, (size_t)0, m, blk, norms, (size_t)0, m, n, np, ntiles, nsplit, nqb, meta, pd, pi, pT, nq_pad,
-                           (unsigned long long*)qthr, 7 | (7 << 8));
+                           (unsigned long long*)qthr, 7 | (7 << 8), 0);
     CK(hipEventRecord(e0));
     for (int r = 0; r < reps; r++) {
         if (qthr) knn_launch_fill_inf(qthr, nq_pad, 0);
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<double, KNN_KL, KNN_KP, EPI, ABL>), dim3(nqb * nsplit), dim3(512), 0, 0,
                            blk, norms, (size_t)0, m, blk, norms, (size_t)0, m, n, np, ntiles, nsplit, nqb, meta, pd, pi, pT, nq_pad,
-                           (unsigned long long*)qthr, 7 | (7 << 8));
+                           (unsigned long long*)qthr, 7 | (7 << 8), 0);
     }
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
