@@ -496,50 +496,68 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     };
 
     // ---- epilogue of tile t: d^2, threshold filter, insertion ------------
+    // Common case (late in the scan): d^2, one masked-tile test on SGPRs,
+    // the lane minimum against the bound, one ballot.  The per-candidate
+    // pending mask is built only when some lane has a survivor.
     auto epilogue = [&](int t) {
         const LDS_AS T *cng = (const LDS_AS T *)(lds + NST * 32768 + (t & 7) * 1024) + 32 * g;
         const T lim = L[KL - 1] < thr ? L[KL - 1] : thr;
-        // INT mode: d^2 is exact and >= 0, so "S != 0" (serial:86) is d^2 > 0
-        const T zfloor = (mode == KNN_MODE_INT) ? (T)0 : (T)-KNN_INF;
-        // wave-uniform: only the block's last tile has rows >= nc, and only
-        // tiles holding one of this wave's queries contain a self pair
+        // wave-uniform (scalar): only the block's last tile has rows >= nc,
+        // and only tiles holding one of this wave's queries contain a self
+        // pair.  Derived from wave_s, not the VGPR wave index, so it is a
+        // scalar branch -- from the VGPR form hipcc predicated all 32
+        // elements with exec masks (~9 issued instructions each).
         const int row0 = t * KNN_TC;
-        const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 16 * wave;
+        const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 16 * wave_s;
         const bool masked = (row0 + KNN_TC > nc) || (gw0 < gt0 + KNN_TC && gt0 < gw0 + 16);
-        // d^2 overwrites the accumulators in place (no extra registers)
-        unsigned pend_all = 0;
+        T cnr[8][4];
 #pragma unroll
         for (int mt = 0; mt < 8; mt++) {
-            T cnr[4];
             if constexpr (ES == 8) {
                 const dbl2 n01 = ((const LDS_AS dbl2 *)cng)[2 * mt];
                 const dbl2 n23 = ((const LDS_AS dbl2 *)cng)[2 * mt + 1];
-                cnr[0] = n01.x; cnr[1] = n01.y; cnr[2] = n23.x; cnr[3] = n23.y;
+                cnr[mt][0] = n01.x; cnr[mt][1] = n01.y; cnr[mt][2] = n23.x; cnr[mt][3] = n23.y;
             } else {
                 const flt4 n4 = ((const LDS_AS flt4 *)cng)[mt];
-                cnr[0] = n4.x; cnr[1] = n4.y; cnr[2] = n4.z; cnr[3] = n4.w;
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                T v = fma((T)-2, acc[mt][r], qn + cnr[r]);
-                if (masked) {
-                    const int row = row0 + 16 * mt + KT<T>::row(g, r);
-                    v = (row < nc && (long)c_base + row != gq) ? v : (T)KNN_INF;
-                }
-                acc[mt][r] = v;
-                pend_all |= (v <= lim && v > zfloor) ? (1u << (4 * mt + r)) : 0u;
+                cnr[mt][0] = n4.x; cnr[mt][1] = n4.y; cnr[mt][2] = n4.z; cnr[mt][3] = n4.w;
             }
         }
+        // d^2 overwrites the accumulators in place (no extra registers)
+#pragma unroll
+        for (int mt = 0; mt < 8; mt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[mt][r] = fma((T)-2, acc[mt][r], qn + cnr[mt][r]);
+        T lanemin = acc[0][0];
+#pragma unroll
+        for (int mt = 0; mt < 8; mt++)
+#pragma unroll
+            for (int r = (mt == 0 ? 1 : 0); r < 4; r++) lanemin = fmin(lanemin, acc[mt][r]);
+        // zeros (INT-mode exact duplicates) and masked tiles only send the
+        // wave down the slow path, where d^2 > 0 and the row mask are
+        // applied (masking here made hipcc copy all 32 d^2 at the join)
+        bool any = masked || __ballot(lanemin <= lim) != 0ull;   // rare late in the scan
         if constexpr (EPI == 0) {
-            T s = acc[0][0];
+            L[0] = fmin(L[0], lanemin);
+            any = false;
+        }
+        if (any) {
+            // INT mode: d^2 is exact and >= 0, so "S != 0" (serial:86) is d^2 > 0
+            const T zfloor = (mode == KNN_MODE_INT) ? (T)0 : (T)-KNN_INF;
+            unsigned pend_all = 0;
 #pragma unroll
             for (int mt = 0; mt < 8; mt++)
-                s = fmin(s, fmin(fmin(acc[mt][0], acc[mt][1]), fmin(acc[mt][2], acc[mt][3])));
-            L[0] = fmin(L[0], s);
-            pend_all = 0;
-        }
-        const bool any = __ballot(pend_all != 0) != 0ull;   // rare late in the scan
-        if (any) {
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    pend_all |= (acc[mt][r] <= lim && acc[mt][r] > zfloor) ? (1u << (4 * mt + r)) : 0u;
+            if (masked) {
+#pragma unroll
+                for (int mt = 0; mt < 8; mt++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int row = row0 + 16 * mt + KT<T>::row(g, r);
+                        if (!(row < nc && (long)c_base + row != gq)) pend_all &= ~(1u << (4 * mt + r));
+                    }
+            }
             // one wave round per survivor of the busiest lane: each lane
             // takes its lowest pending candidate (= lowest row: the stable
             // tie order) through a 5-level select tree over the 32 d^2
