@@ -499,7 +499,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // Common case (late in the scan): d^2, one masked-tile test on SGPRs,
     // the lane minimum against the bound, one ballot.  The per-candidate
     // pending mask is built only when some lane has a survivor.
-    auto epilogue = [&](int t) {
+    auto epilogue = [&](int t, acc_t (&A)[8]) {
         const LDS_AS T *cng = (const LDS_AS T *)(lds + NST * 32768 + (t & 7) * 1024) + 32 * g;
         const T lim = L[KL - 1] < thr ? L[KL - 1] : thr;
         // wave-uniform (scalar): only the block's last tile has rows >= nc,
@@ -510,28 +510,34 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         const int row0 = t * KNN_TC;
         const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 16 * wave_s;
         const bool masked = (row0 + KNN_TC > nc) || (gw0 < gt0 + KNN_TC && gt0 < gw0 + 16);
-        T cnr[8][4];
+        // d^2 overwrites the accumulators in place; the norms are read in
+        // two halves of 4 m-tiles (one wait each, 16 temporaries)
 #pragma unroll
-        for (int mt = 0; mt < 8; mt++) {
-            if constexpr (ES == 8) {
-                const dbl2 n01 = ((const LDS_AS dbl2 *)cng)[2 * mt];
-                const dbl2 n23 = ((const LDS_AS dbl2 *)cng)[2 * mt + 1];
-                cnr[mt][0] = n01.x; cnr[mt][1] = n01.y; cnr[mt][2] = n23.x; cnr[mt][3] = n23.y;
-            } else {
-                const flt4 n4 = ((const LDS_AS flt4 *)cng)[mt];
-                cnr[mt][0] = n4.x; cnr[mt][1] = n4.y; cnr[mt][2] = n4.z; cnr[mt][3] = n4.w;
+        for (int hh = 0; hh < 2; hh++) {
+            T cnr[4][4];
+#pragma unroll
+            for (int m4 = 0; m4 < 4; m4++) {
+                const int mt = 4 * hh + m4;
+                if constexpr (ES == 8) {
+                    const dbl2 n01 = ((const LDS_AS dbl2 *)cng)[2 * mt];
+                    const dbl2 n23 = ((const LDS_AS dbl2 *)cng)[2 * mt + 1];
+                    cnr[m4][0] = n01.x; cnr[m4][1] = n01.y; cnr[m4][2] = n23.x; cnr[m4][3] = n23.y;
+                } else {
+                    const flt4 n4 = ((const LDS_AS flt4 *)cng)[mt];
+                    cnr[m4][0] = n4.x; cnr[m4][1] = n4.y; cnr[m4][2] = n4.z; cnr[m4][3] = n4.w;
+                }
             }
+#pragma unroll
+            for (int m4 = 0; m4 < 4; m4++)
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    A[4 * hh + m4][r] = fma((T)-2, A[4 * hh + m4][r], qn + cnr[m4][r]);
         }
-        // d^2 overwrites the accumulators in place (no extra registers)
+        T lanemin = A[0][0];
 #pragma unroll
         for (int mt = 0; mt < 8; mt++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) acc[mt][r] = fma((T)-2, acc[mt][r], qn + cnr[mt][r]);
-        T lanemin = acc[0][0];
-#pragma unroll
-        for (int mt = 0; mt < 8; mt++)
-#pragma unroll
-            for (int r = (mt == 0 ? 1 : 0); r < 4; r++) lanemin = fmin(lanemin, acc[mt][r]);
+            for (int r = (mt == 0 ? 1 : 0); r < 4; r++) lanemin = fmin(lanemin, A[mt][r]);
         // zeros (INT-mode exact duplicates) and masked tiles only send the
         // wave down the slow path, where d^2 > 0 and the row mask are
         // applied (masking here made hipcc copy all 32 d^2 at the join)
@@ -548,7 +554,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             for (int mt = 0; mt < 8; mt++)
 #pragma unroll
                 for (int r = 0; r < 4; r++)
-                    pend_all |= (acc[mt][r] <= lim && acc[mt][r] > zfloor) ? (1u << (4 * mt + r)) : 0u;
+                    pend_all |= (A[mt][r] <= lim && A[mt][r] > zfloor) ? (1u << (4 * mt + r)) : 0u;
             if (masked) {
 #pragma unroll
                 for (int mt = 0; mt < 8; mt++)
@@ -567,8 +573,8 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 T v[8];
 #pragma unroll
                 for (int mt = 0; mt < 8; mt++) {
-                    const T lo = b0 ? acc[mt][1] : acc[mt][0];
-                    const T hi = b0 ? acc[mt][3] : acc[mt][2];
+                    const T lo = b0 ? A[mt][1] : A[mt][0];
+                    const T hi = b0 ? A[mt][3] : A[mt][2];
                     v[mt] = b1 ? hi : lo;
                 }
                 const T w0 = b2 ? v[1] : v[0], w1 = b2 ? v[3] : v[2];
@@ -584,7 +590,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             }
         }
 #pragma unroll
-        for (int mt = 0; mt < 8; mt++) acc[mt] = (acc_t){0, 0, 0, 0};
+        for (int mt = 0; mt < 8; mt++) A[mt] = (acc_t){0, 0, 0, 0};
         if (!any) return;
         // shared threshold of the query's 4 lanes: their union holds
         // >= 4(ujm+1) >= k+1 entries <= max_h L_h[ujm], and every lane
@@ -698,7 +704,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 // S3: (p1, mt4-7) on f1 || read (p0, mt0-3) of chunk c+1
                 segment(f1, b1, 1, [&](int j) { rd(cs1, 0, 0, f0, j); }, [&]() { glds1(0); });
             }
-            epilogue(t);
+            epilogue(t, acc);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // no LDS-DMA left in flight
     }

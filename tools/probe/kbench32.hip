@@ -65,7 +65,7 @@ int main(int argc, char** argv)
     CK(hipMalloc(&pT, (size_t)nq_pad * 8)); CK(hipMalloc(&qthr, (size_t)nq_pad * 8));
     const float* b = (const float*)blk;
     const double flop = 2.0 * m * (double)m * n;
-    auto pr = [&](const char* name, float ms) { printf("  %-34s %8.2f ms  %6.1f TF  %5.1f%% of 157.3\n", name, ms, flop / ms / 1e9, flop / ms / 1e9 / 1573.0); };
+    auto pr = [&](const char* name, float ms) { printf("  %-34s %8.2f ms  %6.1f TF  %5.1f%% of 157.3\n", name, ms, flop / ms / 1e9, flop / ms / 1e9 / 1.573); };
     printf("k_dist_topk<float,%d,%d> m=%d n=%d (SIFT-like), best of 2\n", KL, KP, m, n);
     pr("full", run<1>(b, rp, m, n, pd, pi, pT, nq_pad, 2, qthr));
     pr("setprio waves 4-7 (ABL 16)", run<1, 16>(b, rp, m, n, pd, pi, pT, nq_pad, 2, qthr));
