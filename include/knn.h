@@ -192,7 +192,14 @@ KNN_API int knn_ctx_begin(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap, si
                   const double *d_meta, void *stream);
 
 /* Fold one packed corpus block (nc rows, global ids c_base..) into the
- * running neighbour lists.  Blocks may come in any order (ring order). */
+ * running neighbour lists.  Blocks may come in any order (ring order).
+ * Asynchronous and overlapped: the step's distance kernel may start while
+ * earlier steps still run (internal streams), and `stream` is made to wait
+ * for step s - KNN_STEP_LAG only.  So work enqueued on `stream` after step
+ * s returns may overwrite the blocks of steps <= s - KNN_STEP_LAG and no
+ * later one: a ring rotates KNN_STEP_LAG + 2 receive buffers (knn_ring.c,
+ * mpiknn/ring.py).  knn_ctx_end orders `stream` after every step. */
+#define KNN_STEP_LAG 2
 KNN_API int knn_ctx_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
                  size_t c_base, void *stream);
 

@@ -26,6 +26,7 @@
     } while (0)
 
 #define KNN_MAX_SPLITS 15 /* merge kernel: 4*splits + 1 lists <= 64 lanes */
+#define KNN_PSETS 4       /* partial-list sets: step s uses set s % 4   */
 #define KNN_PROF_STEPS 64 /* steps timed between two knn_ctx_end calls */
 
 struct knn_ctx {
@@ -36,12 +37,18 @@ struct knn_ctx {
     int kp, kl;         /* state capacity / per-lane list length serving k */
     int xord;           /* k_dist_topk workgroup order (0 split-major, 1 XCD-grouped) */
     int cus;
-    /* per-step partial lists of k_dist_topk, grown to the largest split
-     * count used so far (part_splits) */
-    int part_splits;
-    double *part_d;
-    int *part_i;
-    double *part_T;
+    /* per-step partial lists of k_dist_topk, KNN_PSETS sets used in turn
+     * (step s+1's distance kernel runs while step s is merged), each
+     * grown to the largest split count used so far with it (part_splits) */
+    int part_splits[KNN_PSETS];
+    double *part_d[KNN_PSETS];
+    int *part_i[KNN_PSETS];
+    double *part_T[KNN_PSETS];
+    /* overlapped step schedule (knn_ctx_step): distance kernels alternate
+     * over two streams, merges run in order on a third */
+    hipStream_t ds[2], ms;
+    hipEvent_t ev_in, ev_d[2], ev_m[KNN_PSETS];
+    int nstep;
     /* per-query filter bound shared by all splits and ring steps */
     double *qthr;
     /* running state per query: KNN_KP x (approx d^2, exact S, idx), T pair */
@@ -59,6 +66,8 @@ struct knn_ctx {
     const double *meta;
     int first_step;
     int nsplit_last;
+    size_t split_nc;    /* choose_splits cache: corpus rows -> split count */
+    int split_best;
     int nfail;
     int mode;
     /* kernel timing (knn_ctx_profile): 3 events per step bracket
@@ -128,9 +137,18 @@ int knn_block_pack(void *d_block, size_t cap, size_t rows, size_t n, const doubl
 
 static void ctx_free_buffers(knn_ctx_t *c)
 {
-    hipFree(c->part_d);
-    hipFree(c->part_i);
-    hipFree(c->part_T);
+    for (int b = 0; b < KNN_PSETS; b++) {
+        hipFree(c->part_d[b]);
+        hipFree(c->part_i[b]);
+        hipFree(c->part_T[b]);
+        if (c->ev_m[b]) hipEventDestroy(c->ev_m[b]);
+    }
+    for (int b = 0; b < 2; b++) {
+        if (c->ds[b]) hipStreamDestroy(c->ds[b]);
+        if (c->ev_d[b]) hipEventDestroy(c->ev_d[b]);
+    }
+    if (c->ms) hipStreamDestroy(c->ms);
+    if (c->ev_in) hipEventDestroy(c->ev_in);
     hipFree(c->qthr);
     hipFree(c->st_d);
     hipFree(c->st_x);
@@ -229,6 +247,17 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     ok &= hipMalloc((void **)&c->fail_list, np * sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->fbound, np * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->mode_dev, sizeof(int)) == hipSuccess;
+    for (int b = 0; b < 2; b++) {
+        ok &= hipStreamCreateWithFlags(&c->ds[b], hipStreamNonBlocking) == hipSuccess;
+        ok &= hipEventCreateWithFlags(&c->ev_d[b], hipEventDisableTiming) == hipSuccess;
+    }
+    for (int b = 0; b < KNN_PSETS; b++)
+        ok &= hipEventCreateWithFlags(&c->ev_m[b], hipEventDisableTiming) == hipSuccess;
+    /* merges are short and gate the next steps: highest priority */
+    int prio_lo = 0, prio_hi = 0;
+    hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    ok &= hipStreamCreateWithPriority(&c->ms, hipStreamNonBlocking, prio_hi) == hipSuccess;
+    ok &= hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         ctx_free_buffers(c);
         free(c);
@@ -270,6 +299,7 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
     c->q_rows_pad = knn_rows_pad(q_cap);
     c->meta = d_meta;
     c->first_step = 1;
+    c->nstep = 0;
     c->nfail = 0;
     HIPCHK(hipMemsetAsync(c->fail_count, 0, sizeof(int), (hipStream_t)stream));
     RCHK(knn_launch_fill_inf(c->qthr, (int)c->nq_pad, stream));
@@ -284,11 +314,44 @@ static size_t split_bytes(const knn_ctx_t *c)
 
 #define KNN_PART_BUDGET ((size_t)2 << 30) /* partial-list bytes above one split */
 
-/* Corpus splits per query block: fill the CUs in whole waves of workgroups
- * (one 512-thread workgroup per CU), keep >= 4 tiles per split, and take
- * the fewest splits within 0.5% of the best fill (each split costs a
- * partial-list pass and its memory, capped at KNN_PART_BUDGET). */
-static int choose_splits(const knn_ctx_t *c, size_t nc)
+/* Makespan of one k_dist_topk launch, in tile times: nqb*nsplit workgroups
+ * in split-major order (long splits first, knn_kernels.hip), each costing
+ * its tiles plus KNN_WG_COST; workgroup i goes to XCD i % 8 and there to the
+ * first free CU (one 512-thread workgroup per CU).  Large grids use the
+ * list-scheduling bound instead of the simulation. */
+#define KNN_XCDS 8
+#define KNN_WG_COST 0.5        /* prologue + partial-list flush, in tiles   */
+#define KNN_MERGE_COST 1e-6    /* k_merge per (query, split), in tiles      */
+static double launch_makespan(long nqb, long ntiles, int s, int cus)
+{
+    const long tb = ntiles / s, tr = ntiles % s;
+    const long w = nqb * s;
+    const int per = cus / KNN_XCDS > 0 ? cus / KNN_XCDS : 1;
+    if (w > 16L * cus || per > 64) {
+        const double work = (double)nqb * ntiles + KNN_WG_COST * w;
+        return work / cus + (tb + (tr ? 1 : 0)) + KNN_WG_COST;
+    }
+    double ms = 0.0;
+    for (int x = 0; x < KNN_XCDS; x++) {
+        double cu[64] = {0};
+        for (long i = x; i < w; i += KNN_XCDS) {
+            const long split = i / nqb;
+            int best = 0;
+            for (int u = 1; u < per; u++)
+                if (cu[u] < cu[best]) best = u;
+            cu[best] += (double)(tb + (split < tr ? 1 : 0)) + KNN_WG_COST;
+        }
+        for (int u = 0; u < per; u++)
+            if (cu[u] > ms) ms = cu[u];
+    }
+    return ms;
+}
+
+/* Corpus splits per query block: the count with the smallest modelled
+ * launch makespan plus merge cost (each split adds a partial list per
+ * query), keeping >= 4 tiles per split and the partial lists within
+ * KNN_PART_BUDGET.  Cached per corpus block size. */
+static int choose_splits(knn_ctx_t *c, size_t nc)
 {
     const char *env = getenv("KNN_SPLITS");
     const long nqb = (long)((c->nq + KNN_TQ - 1) / KNN_TQ);
@@ -297,66 +360,98 @@ static int choose_splits(const knn_ctx_t *c, size_t nc)
         int s = atoi(env);
         return s > KNN_MAX_SPLITS ? KNN_MAX_SPLITS : s;
     }
+    if (c->split_nc == nc && c->split_best > 0) return c->split_best;
     int smax = KNN_MAX_SPLITS;
     const size_t per = split_bytes(c);
     if (per > 0 && KNN_PART_BUDGET / per < (size_t)smax)
         smax = KNN_PART_BUDGET / per > 1 ? (int)(KNN_PART_BUDGET / per) : 1;
-    double eff[KNN_MAX_SPLITS + 1] = {0};
-    double best_eff = 0.0;
+    int best = 1;
+    double best_t = 0.0;
     for (int s = 1; s <= smax; s++) {
         if (s > 1 && ntiles / s < 4) break;
-        const long w = nqb * s;
-        const long rounds = (w + c->cus - 1) / c->cus;
-        eff[s] = (double)w / (double)(rounds * c->cus);
-        if (eff[s] > best_eff) best_eff = eff[s];
+        const double t = launch_makespan(nqb, ntiles, s, c->cus) +
+                         KNN_MERGE_COST * (double)c->nq * s;
+        if (s == 1 || t < best_t * (1.0 - 2e-3)) {
+            best = s;
+            best_t = t;
+        }
     }
-    for (int s = 1; s <= smax; s++)
-        if (eff[s] >= best_eff - 5e-3) return s;
-    return 1;
+    c->split_nc = nc;
+    c->split_best = best;
+    return best;
 }
 
-static int ensure_part_buffers(knn_ctx_t *c, int nsplit)
+static int ensure_part_buffers(knn_ctx_t *c, int nsplit, int set)
 {
-    if (nsplit <= c->part_splits) return KNN_OK;
-    hipFree(c->part_d);
-    hipFree(c->part_i);
-    hipFree(c->part_T);
-    c->part_d = NULL;
-    c->part_i = NULL;
-    c->part_T = NULL;
-    c->part_splits = 0;
+    if (nsplit <= c->part_splits[set]) return KNN_OK;
+    /* the set may still be read by an earlier step's merge */
+    HIPCHK(hipStreamSynchronize(c->ms));
+    hipFree(c->part_d[set]);
+    hipFree(c->part_i[set]);
+    hipFree(c->part_T[set]);
+    c->part_d[set] = NULL;
+    c->part_i[set] = NULL;
+    c->part_T[set] = NULL;
+    c->part_splits[set] = 0;
     const size_t npart = (size_t)nsplit * c->nq_pad * 4 * (size_t)c->kl;
-    if (hipMalloc((void **)&c->part_d, npart * sizeof(double)) != hipSuccess ||
-        hipMalloc((void **)&c->part_i, npart * sizeof(int)) != hipSuccess ||
-        hipMalloc((void **)&c->part_T, (size_t)nsplit * c->nq_pad * sizeof(double)) != hipSuccess)
+    if (hipMalloc((void **)&c->part_d[set], npart * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&c->part_i[set], npart * sizeof(int)) != hipSuccess ||
+        hipMalloc((void **)&c->part_T[set], (size_t)nsplit * c->nq_pad * sizeof(double)) != hipSuccess)
         return KNN_ERR_NOMEM;
-    c->part_splits = nsplit;
+    c->part_splits[set] = nsplit;
     return KNN_OK;
 }
 
+/* Step schedule.  Step s runs k_dist_topk on stream ds[s % 2] into partial
+ * set p = s % 4 and k_merge on stream ms (high priority), in step order:
+ *   ds[s%2]: wait ev_in (the caller's stream at this call: the block has
+ *            arrived, begin() is done) and ev_m[p] (merge s-4 has read the
+ *            partial set), then k_dist_topk(s)              -> ev_d[s%2]
+ *   ms:      wait ev_d[s%2] and ev_in, then k_merge(s)      -> ev_m[p]
+ *   caller:  wait ev_m[(s-2)%4] (step s-2 has finished reading its block)
+ * so k_dist_topk(s) starts while k_dist_topk(s-1) drains its last
+ * workgroups -- a ring step no longer pays its launch tail -- and the
+ * merges (which co-reside with the distance workgroups and so stretch
+ * over the next contraction) have two steps of slack before anything waits
+ * on them.  The caller's stream lags KNN_STEP_LAG = 2 steps: work it
+ * enqueues after step s returns is ordered after step s-2 only, so a ring
+ * rotates KNN_STEP_LAG + 2 receive buffers (knn.h).  knn_ctx_end joins
+ * all. */
 int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, void *stream)
 {
     if (!c || !d_cblock || nc == 0 || nc > c->block_cap) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     const int nsplit = choose_splits(c, nc);
+    const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
     c->nsplit_last = nsplit;
-    RCHK(ensure_part_buffers(c, nsplit));
+    RCHK(ensure_part_buffers(c, nsplit, set));
     const void *cblk = d_cblock;
+    hipStream_t cs = (hipStream_t)stream, ds = c->ds[ds_i];
+    HIPCHK(hipEventRecord(c->ev_in, cs));
+    HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
+    if (c->nstep >= KNN_PSETS) HIPCHK(hipStreamWaitEvent(ds, c->ev_m[set], 0));
     hipEvent_t *ev = NULL;
     if (c->prof_on && c->prof_pending < KNN_PROF_STEPS) {
         ev = &c->prof_ev[3 * c->prof_pending++];
-        HIPCHK(hipEventRecord(ev[0], (hipStream_t)stream));
+        HIPCHK(hipEventRecord(ev[0], ds));
     }
     RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
-                              c->part_d, c->part_i, c->part_T, (int)c->nq_pad, c->qthr, c->xord,
-                              stream));
-    if (ev) HIPCHK(hipEventRecord(ev[1], (hipStream_t)stream));
-    RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d, c->part_i, c->part_T, nsplit, (int)c->nq,
-                          (int)c->nq_pad, c->first_step, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk,
-                          c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n, c->meta, stream));
-    if (ev) HIPCHK(hipEventRecord(ev[2], (hipStream_t)stream));
+                              c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr,
+                              c->xord, ds));
+    if (ev) HIPCHK(hipEventRecord(ev[1], ds));
+    HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
+    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));
+    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_in, 0));
+    RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set], nsplit,
+                          (int)c->nq, (int)c->nq_pad, c->first_step, c->st_d, c->st_x, c->st_i, c->st_T,
+                          c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n, c->meta, c->ms));
+    if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
+    HIPCHK(hipEventRecord(c->ev_m[set], c->ms));
+    if (c->nstep >= KNN_STEP_LAG)
+        HIPCHK(hipStreamWaitEvent(cs, c->ev_m[(c->nstep - KNN_STEP_LAG) % KNN_PSETS], 0));
     c->first_step = 0;
+    c->nstep++;
     return KNN_OK;
 }
 
@@ -365,6 +460,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     if (!c || !d_out || c->first_step) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipStreamWaitEvent(s, c->ev_m[(c->nstep - 1) % KNN_PSETS], 0));   /* the last merge */
     RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
                              (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
                              c->fail_list, c->mode_dev, c->fbound, stream));

@@ -390,8 +390,12 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         qb = blockIdx.x % nqb;
         split = blockIdx.x / nqb;
     }
-    const int t_lo = (int)((long)split * ntiles / nsplit);
-    const int t_hi = (int)((long)(split + 1) * ntiles / nsplit);
+    // long splits first: splits 0..tr-1 take tb+1 tiles, the rest tb, so in
+    // split-major order the longest workgroups are dispatched first and the
+    // short ones fill the tail (knn_engine.c: choose_splits models this)
+    const int tb = ntiles / nsplit, tr = ntiles - tb * nsplit;
+    const int t_lo = split * tb + (split < tr ? split : tr);
+    const int t_hi = t_lo + tb + (split < tr ? 1 : 0);
     const int mode = knn_mode<T>(meta, n);
     const int qrow0 = qb * KNN_TQ;
     const int myq = qrow0 + 16 * wave + j16;          // block-local query row

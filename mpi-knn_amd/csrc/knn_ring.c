@@ -25,13 +25,15 @@
 #include <time.h>
 
 #define KNN_RING_MAX 64
+#define NRX (KNN_STEP_LAG + 2)  /* receive buffers per device */
 
 typedef struct {
     int dev;
     size_t rows, base;          /* own block */
     void *qb;                   /* own packed block: the queries, never overwritten */
-    void *bufa, *bufb;          /* receive buffers (capacity R) */
-    void *cur, *nxt, *spare;    /* rotation roles over qb / bufa / bufb */
+    void *rx[KNN_STEP_LAG + 2]; /* receive buffers (capacity R) */
+    void *cur, *nxt;            /* block being folded / being received */
+    int hop;                    /* hops made: hop h lands in rx[h % NRX] */
     double *src;                /* raw rows of the own block */
     double *meta;               /* reduced meta (8 doubles) */
     knn_neighbour_t *d_out;
@@ -93,15 +95,13 @@ static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int
             for (int g = 0; g < P; g++) {
                 if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
                 if (hipStreamWaitEvent(d[g].cs, d[g].ev_comm, 0) != hipSuccess) return KNN_ERR_HIP;
-                /* the own block (queries) only ever leaves; it is never a
-                 * receive target, so the two other buffers alternate */
-                void *t = d[g].cur;
+                /* the own block (queries) only ever leaves; receives
+                 * rotate over KNN_STEP_LAG + 2 buffers because
+                 * knn_ctx_step orders the compute stream after step
+                 * s - KNN_STEP_LAG only (knn.h) */
                 d[g].cur = d[g].nxt;
-                if (t == d[g].qb) {
-                    d[g].nxt = d[g].spare;
-                } else {
-                    d[g].nxt = t;
-                }
+                d[g].hop++;
+                d[g].nxt = d[g].rx[d[g].hop % NRX];
             }
         }
     }
@@ -142,8 +142,9 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             rc = KNN_ERR_HIP;
             break;
         }
-        if (hipMalloc(&e->qb, bytes) != hipSuccess || hipMalloc(&e->bufa, bytes) != hipSuccess ||
-            hipMalloc(&e->bufb, bytes) != hipSuccess ||
+        int rx_ok = 1;
+        for (int b = 0; b < NRX; b++) rx_ok &= hipMalloc(&e->rx[b], bytes) == hipSuccess;
+        if (!rx_ok || hipMalloc(&e->qb, bytes) != hipSuccess ||
             hipMalloc((void **)&e->src, e->rows * n * sizeof(double)) != hipSuccess ||
             hipMalloc((void **)&e->meta, KNN_META_DOUBLES * sizeof(double)) != hipSuccess ||
             hipMalloc((void **)&e->d_out, e->rows * (size_t)k * sizeof(knn_neighbour_t)) != hipSuccess) {
@@ -170,8 +171,8 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         ring_dev_t *e = &d[g];
         hipSetDevice(g);
         e->cur = e->qb;
-        e->nxt = e->bufa;
-        e->spare = e->bufb;
+        e->hop = 0;
+        e->nxt = e->rx[0];
         rc = knn_block_pack_dt(e->qb, dtype, R, e->rows, n, e->src, KNN_F64,
                                layout == KNN_COLMAJOR ? e->rows : n, layout, e->cs);
         if (!rc && hipMemcpyAsync(e->meta, (char *)e->qb + knn_block_meta_offset_dt(R, n, dtype),
@@ -227,8 +228,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         hipSetDevice(g);
         if (d[g].ctx) knn_ctx_destroy(d[g].ctx);
         hipFree(d[g].qb);
-        hipFree(d[g].bufa);
-        hipFree(d[g].bufb);
+        for (int b = 0; b < NRX; b++) hipFree(d[g].rx[b]);
         hipFree(d[g].src);
         hipFree(d[g].meta);
         hipFree(d[g].d_out);

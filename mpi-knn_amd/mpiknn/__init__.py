@@ -31,6 +31,7 @@ VOTE_SERIAL, VOTE_MPI, VOTE_MAJORITY = 0, 1, 2
 MAX_K = 32          # KNN_MAX_K (fp64)
 MAX_K_F32 = 128     # KNN_MAX_K_F32
 META_DOUBLES = 8
+STEP_LAG = 2        # KNN_STEP_LAG: a ring rotates STEP_LAG + 2 receive buffers
 MODE_NAMES = {0: "int-exact", 1: "gemm+rerank", 2: "exact-scan"}
 
 # every symbol include/knn.h declares (checked by tests/test_abi.py)

@@ -10,9 +10,12 @@ mpi-knn-parallel_blocking.c:122-244 / _non_blocking.c:132-259:
   irecv from g-1) is posted BEFORE step s's kernels, so the transfer runs
   on RCCL's stream while the current block is contracted (the reference
   waits for every hop before computing, SURVEY F10);
-* the own packed block stays resident as the query block; two receive
-  buffers alternate (every rank visits all P blocks exactly once -- the
-  reference visits r, r-2, ..., r-P and never r-1, SURVEY F5);
+* the own packed block stays resident as the query block; STEP_LAG + 2
+  receive buffers rotate (every rank visits all P blocks exactly once --
+  the reference visits r, r-2, ..., r-P and never r-1).  Not
+  two: knn_ctx_step orders the caller's stream after step s - STEP_LAG only
+  (its distance kernels overlap, include/knn.h), so the hop posted at step
+  h may only land in the buffer step h - STEP_LAG - 1 read;
 * the block meta is combined with one all_reduce(MAX) of 8 doubles.
 
 The engine object does the per-block work (GpuEngine: libknn kernels on the
@@ -43,8 +46,8 @@ class GpuEngine:
         self.n, self.R, self.nq, self.k, self.dtype = n, R, nq, k, dtype
         nb = mpiknn.block_bytes(R, n, dtype)
         self.qb = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
-        self.bufa = torch.empty(nb, dtype=torch.uint8, device=self.dev)
-        self.bufb = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+        self.rx = tuple(torch.empty(nb, dtype=torch.uint8, device=self.dev)
+                        for _ in range(mpiknn.STEP_LAG + 2))
         self.meta_off = mpiknn.block_meta_offset(R, n, dtype)
         self.meta = torch.zeros(mpiknn.META_DOUBLES, dtype=torch.float64, device=self.dev)
         self.out = torch.zeros(max(nq, 1) * k * 16, dtype=torch.uint8, device=self.dev)
@@ -101,14 +104,16 @@ def ring_search(dist, torch, engine, rank, P, m, q_base):
         dist.all_reduce(engine.meta, op=dist.ReduceOp.MAX)
     engine.begin(q_base)
 
-    state = {"cur": engine.qb, "nxt": engine.bufa, "spare": engine.bufb}
+    rx = engine.rx
+    state = {"cur": engine.qb, "hop": 0}
 
     def one_pass(off, rescan):
         for s in range(P):
             reqs = []
             if s < P - 1:
+                nxt = rx[state["hop"] % len(rx)]
                 ops = [dist.P2POp(dist.isend, state["cur"], (rank + 1) % P),
-                       dist.P2POp(dist.irecv, state["nxt"], (rank - 1) % P)]
+                       dist.P2POp(dist.irecv, nxt, (rank - 1) % P)]
                 reqs = dist.batch_isend_irecv(ops)
             b = (rank - off - s) % P
             base, rows = blocks[b]
@@ -116,9 +121,8 @@ def ring_search(dist, torch, engine, rank, P, m, q_base):
             for r in reqs:
                 r.wait()
             if s < P - 1:
-                old = state["cur"]
-                state["cur"] = state["nxt"]
-                state["nxt"] = state["spare"] if old is engine.qb else old
+                state["cur"] = nxt
+                state["hop"] += 1
 
     one_pass(0, False)
     unresolved = engine.end()

@@ -113,3 +113,10 @@ def test_no_device_reports_cleanly(knn):
     with pytest.raises(knn.KnnError) as e:
         knn.search(np.ones((5, 3)), 2)
     assert e.value.status == knn.ERR_NODEVICE
+
+
+def test_header_constants_mirrored(knn):
+    """mpiknn mirrors the knn.h constants the ring drivers size buffers by."""
+    import re
+    src = open(os.path.join(ROOT, "include", "knn.h")).read()
+    assert int(re.search(r"#define KNN_STEP_LAG (\d+)", src).group(1)) == knn.STEP_LAG

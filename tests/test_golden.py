@@ -1,0 +1,105 @@
+"""Committed golden fixtures (tests/golden/, made by tests/golden/make_golden.py).
+
+CPU: the oracle reproduces the reference-run aggregates (reference_runs.json,
+SURVEY.md sec.0/sec.4) and the committed neighbour fixtures.  GPU: libknn
+through the C ABI reproduces the same fixtures bit for bit -- digits (integer
+mode), the real-valued digits variant (GEMM filter + exact re-rank) and 48
+sampled queries of the full 60000x784 MNIST-shaped corpus (configs[1]).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import datasets
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    with np.load(os.path.join(GOLD, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def runs():
+    with open(os.path.join(GOLD, "reference_runs.json")) as f:
+        return json.load(f)
+
+
+def check_digits(nb, g):
+    assert np.array_equal(nb["idx"], g["idx"].astype(np.int32))
+    assert np.array_equal(nb["distance"], np.sqrt(g["d2"].astype(np.float64)))
+
+
+def check_digits_real(nb, g):
+    assert np.array_equal(nb["idx"], g["idx"].astype(np.int32))
+    assert np.array_equal(nb["distance"].view(np.uint64), g["dist_bits"])
+
+
+def check_mnist_rows(nb_rows, g):
+    assert np.array_equal(nb_rows["idx"], g["idx"])
+    assert np.array_equal(nb_rows["distance"], np.sqrt(g["d2"].astype(np.float64)))
+
+
+def test_oracle_reference_runs(oracle):
+    r = runs()
+    X, y = datasets.digits()
+    nb = oracle.knn(X, 30)
+    assert oracle.classify(nb, y, 10, oracle.VOTE_SERIAL)[1] == r["digits"]["matches_serial_rule"]
+    assert oracle.classify(nb, y, 10, oracle.VOTE_MPI)[1] == r["digits"]["matches_mpi_rule"]
+    assert oracle.classify(nb, y, 10, oracle.VOTE_MAJORITY)[1] == \
+        r["digits"]["matches_true_majority"]
+    Xr, yr = datasets.digits_real()
+    nbr = oracle.knn(Xr, 30)
+    assert oracle.classify(nbr, yr, 10, oracle.VOTE_SERIAL)[1] == \
+        r["digits_real"]["matches_serial_rule"]
+
+
+def test_oracle_matches_fixtures(oracle):
+    X, y = datasets.digits()
+    nb = oracle.knn(X, 30)
+    g = load("digits_k30.npz")
+    check_digits(nb, g)
+    pred, _ = oracle.classify(nb, y, 10, oracle.VOTE_SERIAL)
+    assert np.array_equal(np.asarray(pred), g["pred"].astype(np.asarray(pred).dtype))
+    check_digits_real(oracle.knn(datasets.digits_real()[0], 30), load("digits_real_k30.npz"))
+
+
+def test_oracle_matches_mnist_sample(oracle):
+    g = load("mnist_like_sample.npz")
+    X, _ = datasets.mnist_like(60000)
+    rows = g["rows"][::6]                        # a subset keeps the CPU suite quick
+    got = np.concatenate([oracle.knn(X, 30, rows=(int(r), 1)) for r in rows])
+    check_mnist_rows(got, {"idx": g["idx"][::6], "d2": g["d2"][::6]})
+
+
+@pytest.mark.gpu
+def test_gpu_digits_fixture(knn):
+    X, y = datasets.digits()
+    nb, _ = knn.search(X, 30)
+    g = load("digits_k30.npz")
+    check_digits(nb, g)
+    pred, matches = knn.classify(nb, y, 10, knn.VOTE_SERIAL)
+    assert matches == runs()["digits"]["matches_serial_rule"]
+    assert np.array_equal(np.asarray(pred), g["pred"].astype(np.asarray(pred).dtype))
+
+
+@pytest.mark.gpu
+def test_gpu_digits_real_fixture(knn):
+    nb, _ = knn.search(datasets.digits_real()[0], 30)
+    check_digits_real(nb, load("digits_real_k30.npz"))
+
+
+@pytest.mark.gpu
+def test_gpu_mnist_full_size_fixture(knn):
+    """configs[1] at full size (60000x784 fp64, k=30, col-major like the
+    .mat); the 48 committed rows are compared bit-exact."""
+    X, _ = datasets.mnist_like(60000)
+    nb, _ = knn.search(np.asfortranarray(X), 30, layout="col")
+    g = load("mnist_like_sample.npz")
+    check_mnist_rows(nb[g["rows"]], g)
+    # size-independent properties over all 60000 rows: sorted, no self, no S=0
+    d = nb["distance"]
+    assert np.all(d[:, 1:] >= d[:, :-1]) and np.all(d > 0)
+    assert not np.any(nb["idx"] == np.arange(1, 60001)[:, None])

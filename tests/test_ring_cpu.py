@@ -24,8 +24,7 @@ class CpuEngine:
         self.O = oracle
         self.n, self.R, self.nq, self.k = n, R, nq, k
         self.qb = torch.zeros((R, n + 1), dtype=torch.float64)   # last column: row count
-        self.bufa = torch.zeros_like(self.qb)
-        self.bufb = torch.zeros_like(self.qb)
+        self.rx = tuple(torch.zeros_like(self.qb) for _ in range(4))
         self.meta = torch.zeros(8, dtype=torch.float64)
         self.force_rescan = force_rescan
         self.visits = {False: [], True: []}
