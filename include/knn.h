@@ -223,11 +223,13 @@ KNN_API int knn_search_packed(knn_ctx_t *ctx, const void *d_block, size_t m,
  * 1 fp64 GEMM + exact re-rank, 2 exact scan) and the corpus split count. */
 KNN_API int knn_ctx_info(const knn_ctx_t *ctx, int *mode, int *splits);
 
-/* Kernel timing with HIP events on the launch stream (the timers of
+/* Kernel timing with HIP events on the launch streams (the timers of
  * serial:70-98 at kernel granularity).  enable = 1 starts recording and
- * zeroes the totals, 0 stops (totals kept), -1 only reads.  Totals (ms) cover every
- * k_dist_topk / k_merge launch since the last reset whose knn_ctx_end has
- * returned; *launches counts k_dist_topk launches. */
+ * zeroes the totals, 0 stops (totals kept), -1 only reads.  Totals (ms) cover
+ * every step since the last reset whose knn_ctx_end has returned: dist_ms is
+ * the time during which some k_dist_topk runs (the union of their
+ * intervals per search -- steps overlap, knn_ctx_step), merge_ms the time
+ * k_merge work adds outside it; *launches counts k_dist_topk launches. */
 KNN_API int knn_ctx_profile(knn_ctx_t *ctx, int enable, double *dist_ms, double *merge_ms,
                     int *launches);
 

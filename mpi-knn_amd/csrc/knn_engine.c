@@ -187,17 +187,44 @@ int knn_ctx_profile(knn_ctx_t *c, int enable, double *dist_ms, double *merge_ms,
     return KNN_OK;
 }
 
-/* after the stream has been synchronised: fold the recorded steps */
+/* after the stream has been synchronised: fold the recorded steps of one
+ * search.  Step i has events [3i] (distance kernel may start), [3i+1]
+ * (distance kernel done), [3i+2] (merge done); overlapping steps are
+ * counted once: dist = union of [3i, 3i+1], merge = union of [3i+1, 3i+2]
+ * minus the distance union. */
+static double interval_union(double *st, double *en, int n)
+{
+    for (int i = 1; i < n; i++)  /* insertion sort by start (n <= 64) */
+        for (int j = i; j > 0 && st[j] < st[j - 1]; j--) {
+            double t = st[j]; st[j] = st[j - 1]; st[j - 1] = t;
+            t = en[j]; en[j] = en[j - 1]; en[j - 1] = t;
+        }
+    double total = 0.0, end = -1e30;
+    for (int i = 0; i < n; i++) {
+        const double s0 = st[i] > end ? st[i] : end;
+        if (en[i] > s0) total += en[i] - s0;
+        if (en[i] > end) end = en[i];
+    }
+    return total;
+}
+
 static int prof_collect(knn_ctx_t *c)
 {
-    for (int i = 0; i < c->prof_pending; i++) {
-        float a = 0.f, b = 0.f;
-        HIPCHK(hipEventElapsedTime(&a, c->prof_ev[3 * i], c->prof_ev[3 * i + 1]));
-        HIPCHK(hipEventElapsedTime(&b, c->prof_ev[3 * i + 1], c->prof_ev[3 * i + 2]));
-        c->prof_dist_ms += a;
-        c->prof_merge_ms += b;
-        c->prof_launches++;
+    const int n = c->prof_pending;
+    double ds[KNN_PROF_STEPS], de[KNN_PROF_STEPS], as[KNN_PROF_STEPS], ae[KNN_PROF_STEPS];
+    for (int i = 0; i < n; i++) {
+        float s = 0.f, e = 0.f, me = 0.f;
+        HIPCHK(hipEventElapsedTime(&s, c->prof_ev[0], c->prof_ev[3 * i]));
+        HIPCHK(hipEventElapsedTime(&e, c->prof_ev[0], c->prof_ev[3 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&me, c->prof_ev[0], c->prof_ev[3 * i + 2]));
+        ds[i] = as[i] = s;
+        de[i] = e;
+        ae[i] = me;
     }
+    const double dist = interval_union(ds, de, n), all = interval_union(as, ae, n);
+    c->prof_dist_ms += dist;
+    c->prof_merge_ms += all > dist ? all - dist : 0.0;
+    c->prof_launches += n;
     c->prof_pending = 0;
     return KNN_OK;
 }

@@ -69,8 +69,11 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
         dist_ms, merge_ms, launches = eng.ctx.profile(0)
-        res[P] = {"rank_ms": dt * 1e3, "dist_ms_per_launch": dist_ms / max(launches, 1),
-                  "merge_ms_per_pass": merge_ms / args.steps, "splits": eng.ctx.info()[1]}
+        flops = 2.0 * blocks[0][1] * m * n * args.steps
+        res[P] = {"rank_ms": dt * 1e3, "dist_busy_ms_per_pass": dist_ms / args.steps,
+                  "dist_tflops": flops / (dist_ms * 1e-3) / 1e12 if dist_ms > 0 else None,
+                  "exposed_merge_ms_per_pass": merge_ms / args.steps,
+                  "splits": eng.ctx.info()[1]}
         del bufs, eng
         torch.cuda.empty_cache()
     t1 = res[min(res)]["rank_ms"]
