@@ -108,6 +108,19 @@ KNN_API int knn_search(const double *X, size_t m, size_t n, int layout,
                const double *labels, int k, int ngpus, int dtype,
                knn_neighbour_t *out);
 
+/* Bug-compatible mode (opt-in): the lists mpi-knn-parallel_
+ * blocking.c / _non_blocking.c with `procs` ranks actually compute.  Rank
+ * r keeps R = floor(m/procs) rows (the rest dropped, blk:81), folds its own
+ * block, then the blocks of ranks r-2, r-3, ..., r-procs (= r again), each
+ * truncated by the short first hop (blk:130-146: last ~2R/(n+2) rows zero)
+ * and carrying idx 0 / label 0 (blk:169,231); block r-1 is never seen.
+ * Ties keep scan order (blk:24-31).  fp64, k <= KNN_MAX_K, procs >= 2; the
+ * ranks run one after another on device 0.  out: procs*R*k records, rank r
+ * at out + r*R*k.  labels (nullable) fill .label of own-block records. */
+KNN_API int knn_search_mpi_compat(const double *X, size_t m, size_t n, int layout,
+                                  const double *labels, int k, int procs,
+                                  knn_neighbour_t *out);
+
 /* Search wall time of the last knn_search() on this thread, seconds: the
  * span the reference times (serial:70-98, blk:120-250) -- device compute
  * only, excluding load, H2D, D2H and vote. */

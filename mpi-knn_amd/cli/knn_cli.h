@@ -9,6 +9,8 @@
  * (serial:40, blk:65) unless KNN_MAT names another file; variables
  * train_X / train_labels (serial:47,52).  P selects the GPU count (one GPU
  * per reference rank); T (OpenMP threads) has no GPU meaning and is ignored.
+ * KNN_MPI_COMPAT=1 makes the MPI mains print what the reference MPI
+ * programs compute, bugs included (knn_search_mpi_compat).
  */
 #ifndef KNN_CLI_H
 #define KNN_CLI_H
@@ -35,7 +37,7 @@ static int cli_fail(const char *what, int rc)
 }
 
 /* load + search; returns 0 or a process exit code */
-static int cli_search(cli_run_t *r, int ngpus)
+static int cli_search(cli_run_t *r, int ngpus, int compat)
 {
     const char *path = getenv("KNN_MAT");
     if (!path || !*path) path = "mnist_train.mat";
@@ -47,8 +49,15 @@ static int cli_search(cli_run_t *r, int ngpus)
     }
     r->nb = (knn_neighbour_t *)malloc(r->m * NN * sizeof(knn_neighbour_t));
     if (!r->nb) return cli_fail("malloc", KNN_ERR_NOMEM);
-    rc = knn_search(r->X, r->m, r->n, KNN_COLMAJOR, r->labels, NN, ngpus, KNN_F64, r->nb);
-    if (rc) return cli_fail("knn_search", rc);
+    if (compat) {
+        /* ngpus = the reference's procs; rows past procs*floor(m/procs) dropped */
+        rc = knn_search_mpi_compat(r->X, r->m, r->n, KNN_COLMAJOR, r->labels, NN, ngpus, r->nb);
+        if (rc) return cli_fail("knn_search_mpi_compat", rc);
+        r->m = (r->m / (size_t)ngpus) * (size_t)ngpus;
+    } else {
+        rc = knn_search(r->X, r->m, r->n, KNN_COLMAJOR, r->labels, NN, ngpus, KNN_F64, r->nb);
+        if (rc) return cli_fail("knn_search", rc);
+    }
     r->seconds = knn_last_search_seconds();
     return 0;
 }
@@ -73,9 +82,11 @@ __attribute__((unused)) static int cli_mpi_main(int argc, char **argv, int nonbl
     if (procs < 1) procs = 1;
     cli_run_t r;
     memset(&r, 0, sizeof(r));
-    int ec = cli_search(&r, procs);
+    const char *cenv = getenv("KNN_MPI_COMPAT");
+    const int compat = cenv && cenv[0] == '1' && procs >= 2;
+    int ec = cli_search(&r, procs, compat);
     if (ec) return ec;
-    const size_t R = (r.m + procs - 1) / procs;
+    const size_t R = (r.m + procs - 1) / procs;   /* compat: r.m = procs*floor(m/procs) */
     int *pred = (int *)malloc(r.m * sizeof(int));
     size_t total = 0;
     int rc = pred ? knn_classify(r.nb, r.m, NN, MAXC, KNN_VOTE_MPI, r.labels, pred, &total)

@@ -12,7 +12,7 @@ int main(int argc, char *argv[])
     cli_run_t r;
     memset(&r, 0, sizeof(r));
     printf("Number of Classes: %d\n", MAXC);                          /* serial:65 */
-    int ec = cli_search(&r, 1);
+    int ec = cli_search(&r, 1, 0);
     if (ec) return ec;
     printf("Sorting done\nClock time = %f\n", r.seconds);             /* serial:98 */
     size_t matches = 0;

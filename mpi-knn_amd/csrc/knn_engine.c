@@ -98,6 +98,7 @@ const char *knn_strerror(int status)
 void knn_free(void *p) { free(p); }
 
 double knn_last_search_seconds(void) { return g_last_search_s; }
+void knn_set_last_search_seconds(double s) { g_last_search_s = s; }
 
 static int dtype_ok(int dtype) { return dtype == KNN_F64 || dtype == KNN_F32; }
 

@@ -95,4 +95,7 @@ int knn_launch_vote(knn_neighbour_t *nb, size_t m, int k, int nclasses, int rule
 #ifdef __cplusplus
 }
 #endif
+/* knn_engine.c: the value knn_last_search_seconds() returns (this thread) */
+void knn_set_last_search_seconds(double s);
+
 #endif

@@ -41,7 +41,7 @@ API_SYMBOLS = (
     "knn_ctx_create", "knn_ctx_destroy", "knn_ctx_begin", "knn_ctx_step", "knn_ctx_end",
     "knn_ctx_rescan_step", "knn_ctx_rescan_end", "knn_search_packed", "knn_ctx_info",
     "knn_ctx_profile", "knn_block_bytes_dt", "knn_block_meta_offset_dt", "knn_block_pack_dt",
-    "knn_ctx_create_dt", "knn_classify_device",
+    "knn_ctx_create_dt", "knn_classify_device", "knn_search_mpi_compat",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -79,6 +79,7 @@ def _load():
         "knn_load_mat": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, pp, psz, psz, pp, psz], i),
         "knn_free": ([p], None),
         "knn_search": ([p, sz, sz, i, p, i, i, i, p], i),
+        "knn_search_mpi_compat": ([p, sz, sz, i, p, i, i, p], i),
         "knn_last_search_seconds": ([], d),
         "knn_classify": ([p, sz, i, i, i, p, p, psz], i),
         "knn_block_bytes": ([sz, sz], sz),
@@ -169,6 +170,24 @@ def search(X, k=30, ngpus=1, labels=None, layout="row", dtype="f64"):
     rc = lib.knn_search(_ptr(buf), m, n, lay, _ptr(lab), k, ngpus, DTYPES[dtype], _ptr(out))
     _check(rc, "knn_search")
     return out, lib.knn_last_search_seconds()
+
+
+def search_mpi_compat(X, k=30, procs=2, labels=None, layout="row"):
+    """knn_search_mpi_compat: the lists the reference MPI programs compute
+    with `procs` ranks, bugs included (include/knn.h).  Returns
+    (neighbours (procs*floor(m/procs), k) NB_DTYPE, search seconds)."""
+    X = np.asarray(X, dtype=np.float64)
+    m, n = X.shape
+    if layout == "col":
+        buf, lay = np.asfortranarray(X), COLMAJOR
+    else:
+        buf, lay = np.ascontiguousarray(X), ROWMAJOR
+    R = m // procs if procs > 0 else 0
+    out = np.zeros((max(procs * R, 1), k), dtype=NB_DTYPE)
+    lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.float64)
+    rc = lib.knn_search_mpi_compat(_ptr(buf), m, n, lay, _ptr(lab), k, procs, _ptr(out))
+    _check(rc, "knn_search_mpi_compat")
+    return out[: procs * R], lib.knn_last_search_seconds()
 
 
 def classify(nb, labels, nclasses=10, rule=VOTE_SERIAL):

@@ -95,6 +95,54 @@ def knn_block(Q, q_base, C, c_base, lists, labels=None, nthreads=0):
     return lists
 
 
+def mpi_compat(X, k=30, procs=2, labels=None):
+    """What the reference MPI programs compute with `procs` ranks (SURVEY
+    F5), restated from mpi-knn-parallel_blocking.c with the block fold above:
+
+    * R = floor(m/procs) rows per rank, the remainder dropped (blk:81);
+    * step 0 folds the rank's OWN block, real ids/labels (blk:155-181,
+      matrix[i] not matrix_temp[i]; ids/labels blk:107-108);
+    * the first hop sends R*n of R*(n+2) doubles (blk:130,137,146): the
+      receiver's (n+2)-strided rows below q = R*n // (n+2) arrive whole,
+      row q its first R*n - q*(n+2) doubles, later rows stay zero;
+    * matrix_send copies only the n feature columns (blk:169,231): every
+      forwarded block has id 0 / label 0 and keeps the truncation;
+    * iteration p = 0..procs-2 (blk:187-244) folds block r-2-p.
+    Ties keep scan order (strict <, stable distance-only qsort, blk:24-31):
+    visits get scan-order ids (own block real ids, visit p m + p*R + row),
+    then ids above m become idx 0 / label 0.
+    """
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    m, n = X.shape
+    P = procs
+    R = m // P
+    out = np.zeros((P * R, k), dtype=NB_DTYPE)
+
+    def trunc(b):
+        B = X[b * R:(b + 1) * R].copy()
+        sent, stride = R * n, n + 2
+        q = sent // stride
+        for i in range(q, R):
+            got = sent - q * stride if i == q else 0
+            B[i, min(got, n):] = 0.0
+        return B
+
+    for r in range(P):
+        Q = X[r * R:(r + 1) * R]
+        L = lists_init(R, k)
+        knn_block(Q, r * R, Q, r * R, L)
+        for p in range(P - 1):
+            knn_block(Q, r * R, trunc((r - 2 - p) % P), m + p * R, L)
+        fwd = L["idx"] > m
+        L["idx"][fwd] = 0
+        L["label"] = 0
+        own = L["idx"] > 0
+        if labels is not None:
+            L["label"][own] = np.asarray(labels)[L["idx"][own] - 1].astype(np.int32)
+        out[r * R:(r + 1) * R] = L
+    return out
+
+
 def classify(nb, labels, nclasses=10, rule=VOTE_SERIAL, q0=0):
     """Vote + Matches (serial:104-130 / blk:252-270).  Returns (pred, matches)."""
     nb = np.ascontiguousarray(nb)

@@ -16,13 +16,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "mpi-knn_amd", "bin")
 
 
-def _run(tmp_path, exe, args=(), compress=True):
+def _run(tmp_path, exe, args=(), compress=True, extra_env=None):
     X, y = datasets.digits()
     path = tmp_path / "mnist_train.mat"
     scipy.io.savemat(str(path), {"train_X": X, "train_labels": y.reshape(-1, 1)},
                      do_compression=compress)
     env = dict(os.environ)
     env.pop("KNN_MAT", None)
+    env.pop("KNN_MPI_COMPAT", None)
+    env.update(extra_env or {})
     r = subprocess.run([os.path.join(BIN, exe)] + list(args), cwd=str(tmp_path), env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
@@ -60,3 +62,21 @@ def test_mpi_blocking_multi_gpu(tmp_path):
     out = _run(tmp_path, "mpi-knn-parallel_blocking", [str(ng), "1"])
     counts = [int(v) for v in re.findall(r"Matches: (\d+)", out)]
     assert sum(counts) == 1635 and len(counts) == ng
+
+
+@pytest.mark.parametrize("exe,fmt", [("mpi-knn-parallel_blocking", r"Matches: (\d+)"),
+                                     ("mpi-knn-parallel_non_blocking", r"Matches(\d+)")])
+def test_mpi_bug_compat_mode(tmp_path, exe, fmt):
+    """KNN_MPI_COMPAT=1: per-rank Matches of the reference's own (F5) lists,
+    against the oracle's restatement + the MPI vote rule."""
+    import oracle
+    X, y = datasets.digits()
+    P = 3
+    out = _run(tmp_path, exe, [str(P), "1"], extra_env={"KNN_MPI_COMPAT": "1"})
+    counts = [int(v) for v in re.findall(fmt, out)]
+    nb = oracle.mpi_compat(X, 30, P, labels=y)
+    R = X.shape[0] // P
+    pred, _ = oracle.classify(nb, y, 10, oracle.VOTE_MPI)
+    want = [int((np.asarray(pred[r * R:(r + 1) * R]) == y[r * R:(r + 1) * R]).sum())
+            for r in range(P)]
+    assert counts == want
