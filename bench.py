@@ -34,6 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-knn_amd"))
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix (spec; 78.2 measured, tools/probe)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix (spec, MI355X_MICROARCH.md; 155 measured)
+FP16_MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 matrix (spec ~2.5 PF, MI355X_MICROARCH.md)
 
 WORKLOADS = {
     # name: (m, n, k, dtype, layout_col, description)
@@ -156,6 +157,7 @@ def main():
         elapsed = float(t.item())
     dist_ms, merge_ms, launches = engine.ctx.profile(0)
     mode, splits = engine.ctx.info()
+    cbits = engine.ctx.contraction_bits()
 
     # parity spot-check of this rank's first queries against the oracle
     check = None
@@ -187,13 +189,17 @@ def main():
         traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
-    peak = FP64_MFMA_PEAK_TFLOPS if dtype == "f64" else FP32_MFMA_PEAK_TFLOPS
+    # the MFMA the contraction ran on: fp32 searches on exactly representable
+    # 8-bit-style integer data contract on fp16 MFMA (include/knn.h)
+    peak = {64: FP64_MFMA_PEAK_TFLOPS, 32: FP32_MFMA_PEAK_TFLOPS,
+            16: FP16_MFMA_PEAK_TFLOPS}[cbits]
     roofline = {
         "kernel": "k_dist_topk",
         "bound": "mfma",
         "achieved": achieved,
         "peak": peak,
         "unit": "TFLOP/s",
+        "mfma_input": {64: "f64", 32: "f32", 16: "f16 (exact on this data)"}[cbits],
         "frac": (achieved / peak) if achieved else None,
         "traffic": traffic,
         # distance-stage busy time (union of the overlapped k_dist_topk

@@ -236,6 +236,13 @@ KNN_API int knn_search_packed(knn_ctx_t *ctx, const void *d_block, size_t m,
  * 1 fp64 GEMM + exact re-rank, 2 exact scan) and the corpus split count. */
 KNN_API int knn_ctx_info(const knn_ctx_t *ctx, int *mode, int *splits);
 
+/* Input width in bits of the MFMA contraction of the current search: 64
+ * (fp64 blocks), 32 (fp32 blocks), or 16 when an fp32 search runs its
+ * contraction on fp16 MFMA because that is exact for its data (integers
+ * with max|x| <= 2048 in the fp32 exact-integer range; set by
+ * knn_ctx_begin; KNN_NO_H16=1 disables it).  0 for a NULL context. */
+KNN_API int knn_ctx_contraction_bits(const knn_ctx_t *ctx);
+
 /* Kernel timing with HIP events on the launch streams (the timers of
  * serial:70-98 at kernel granularity).  enable = 1 starts recording and
  * zeroes the totals, 0 stops (totals kept), -1 only reads.  Totals (ms) cover

@@ -36,6 +36,7 @@ struct knn_ctx {
     int k;
     int kp, kl;         /* state capacity / per-lane list length serving k */
     int xord;           /* k_dist_topk workgroup order (0 split-major, 1 XCD-grouped) */
+    int h16;            /* this search's fp32 contraction runs on fp16 MFMA (exact) */
     int cus;
     /* per-step partial lists of k_dist_topk, KNN_PSETS sets used in turn
      * (step s+1's distance kernel runs while step s is merged), each
@@ -309,12 +310,31 @@ int knn_ctx_destroy(knn_ctx_t *c)
     return KNN_OK;
 }
 
+int knn_ctx_contraction_bits(const knn_ctx_t *c)
+{
+    if (!c) return 0;
+    return c->dtype == KNN_F64 ? 64 : (c->h16 ? 16 : 32);
+}
+
 int knn_ctx_info(const knn_ctx_t *c, int *mode, int *splits)
 {
     if (!c) return KNN_ERR_INVALID;
     if (mode) *mode = c->mode;
     if (splits) *splits = c->nsplit_last;
     return KNN_OK;
+}
+
+/* fp32 INT mode (knn_mode<float>: integers, n max|x|^2 <= 2^23,
+ * n range^2 <= 2^24) with max|x| <= 2048, so every value is exact in fp16:
+ * the fp16 MFMA contraction gives the fp32 path's dot products bit for bit
+ * (knn_kernels.hip, knn_to_h8). */
+static int knn_h16_exact(const double *meta, size_t n)
+{
+    if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e37)) return 0;
+    const double mx = meta[KNN_META_MAXABS];
+    const double rg = meta[KNN_META_MAXPOS] + meta[KNN_META_MAXNEG];
+    return meta[KNN_META_NONINT] == 0.0 && mx <= 2048.0 && (double)n * mx * mx <= 8388608.0 &&
+           (double)n * rg * rg <= 16777216.0;
 }
 
 int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_base,
@@ -329,6 +349,18 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
     c->first_step = 1;
     c->nstep = 0;
     c->nfail = 0;
+    c->h16 = 0;
+    if (c->dtype == KNN_F32) {
+        /* one 64-byte read of the reduced meta per search picks the
+         * contraction: fp16 MFMA when it is exact (knn_h16_exact) */
+        const char *off = getenv("KNN_NO_H16");
+        if (!(off && off[0] == '1')) {
+            double hm[KNN_META_DOUBLES];
+            HIPCHK(hipMemcpyAsync(hm, d_meta, sizeof(hm), hipMemcpyDeviceToHost, (hipStream_t)stream));
+            HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+            c->h16 = knn_h16_exact(hm, c->n);
+        }
+    }
     HIPCHK(hipMemsetAsync(c->fail_count, 0, sizeof(int), (hipStream_t)stream));
     RCHK(knn_launch_fill_inf(c->qthr, (int)c->nq_pad, stream));
     return KNN_OK;
@@ -466,7 +498,7 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
                               c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr,
-                              c->xord, ds));
+                              (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0), ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
     HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));

@@ -62,6 +62,22 @@ template <> struct KT<float> {
 };
 template <typename T> static constexpr int knn_bk() { return 128 / (int)sizeof(T); }
 
+// fp16 contraction of fp32 blocks (H16): INT-mode data with |x| <= 2048 is
+// exact in fp16, every product exact in fp32 and every partial sum an
+// integer <= n max|x|^2 <= 2^23, so v_mfma_f32_16x16x32_f16 yields the same
+// dot products as the fp32 MFMA chain, bit for bit, in any summation order.
+// Lane (row, g) converts its two 16-byte fp32 slots of a chunk (features
+// 4g..4g+3 of pieces 0 and 1) into one 8-half operand; the query side is
+// converted identically, so each chunk's 32 features are summed once.
+typedef _Float16 knn_h8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ knn_h8 knn_to_h8(flt4 a, flt4 b)
+{
+    knn_h8 r;
+    r[0] = (_Float16)a.x; r[1] = (_Float16)a.y; r[2] = (_Float16)a.z; r[3] = (_Float16)a.w;
+    r[4] = (_Float16)b.x; r[5] = (_Float16)b.y; r[6] = (_Float16)b.z; r[7] = (_Float16)b.w;
+    return r;
+}
+
 // ---------------------------------------------------------------------------
 // Mode decision from the max-reduced meta (identical on every rank).
 //   INT : every value an integer and every partial sum of the GEMM form
@@ -356,7 +372,7 @@ __device__ __forceinline__ void glds4(const void *src, unsigned lds_dst)
 // from the split's first tile (L2-resident; wrong results), 11 each
 // segment's load before its first MFMA pair, 13 waves 0..3 stage for all
 // eight.  libknn instantiates <.., 1, 0>.
-template <typename T, int KL, int KS, int EPI = 1, int ABL = 0>
+template <typename T, int KL, int KS, int EPI = 1, int ABL = 0, int H16 = 0>
 __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const T *__restrict__ qblk, const T *__restrict__ qnorm, size_t q_base, int nq,
     const T *__restrict__ cblk, const T *__restrict__ cnorm, size_t c_base, int nc,
@@ -684,6 +700,35 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             gnorm(t + 2, t + 2);
             for (int fc = 0; fc < nfc; fc++, c++) {
                 LDS_AS char *cs = cs_of(c);
+                if constexpr (H16 != 0) {
+                    // fp16 MFMA on converted fp32 fragments (knn_to_h8): one
+                    // 16x16x32 per m-tile per chunk.  Same staging sequence
+                    // as below: loads 1..3 of chunk c+3, the chunk barrier,
+                    // then load 0 of chunk c+4 into the freed stage.
+                    glds1(1);
+                    glds1(2);
+                    glds1(3);
+                    const knn_h8 bh = knn_to_h8(rdq(cs, 0), rdq(cs, 1));
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            rd(cs, 0, h, f0, j);
+                            rd(cs, 1, h, f1, j);
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            acc[4 * h + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                                knn_to_h8(f0[j], f1[j]), bh, acc[4 * h + j], 0, 0, 0);
+                    }
+                    advance();
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    if constexpr (SELF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    glds1(0);
+                    continue;
+                }
                 // one staging load per segment, mid-segment: loads 1..3 of
                 // chunk c+3 in S0..S2, load 0 of chunk c+4 in S3 (after the
                 // barrier that freed its stage).  All 8 waves issuing right
@@ -1297,8 +1342,9 @@ template <typename T, int KL, int KP>
 static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int nq, const T *cblk,
                             size_t c_rows_pad, size_t c_base, int nc, int n, const double *meta,
                             int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
-                            double *qthr, int k, int xord, hipStream_t s)
+                            double *qthr, int k, int flags, hipStream_t s)
 {
+    const int xord = flags & 1;
     constexpr int dt = sizeof(T) == 8 ? KNN_F64 : KNN_F32;
     const int np = (int)knn_n_pad_dt(n, dt);
     const int nqb = (nq + KNN_TQ - 1) / KNN_TQ;
@@ -1318,10 +1364,19 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     const T *qnorm = qblk + q_rows_pad * np;
     const T *cnorm = cblk + c_rows_pad * np;
     const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP>), dim3((unsigned)(nqb_grid * nsplit)),
-                       dim3(512), 0, s, qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np,
-                       ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                       (unsigned long long *)qthr, uj, xord);
+    const dim3 grid((unsigned)(nqb_grid * nsplit));
+    if constexpr (sizeof(T) == 4) {
+        if (flags & KNN_DIST_H16) {   // host-checked: INT mode and max|x| <= 2048
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 0, 1>), grid, dim3(512), 0, s,
+                               qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles, nsplit,
+                               nqb, meta, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr,
+                               uj, xord);
+            return hip_status();
+        }
+    }
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP>), grid, dim3(512), 0, s, qblk, qnorm,
+                       q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles, nsplit, nqb, meta, part_d,
+                       part_i, part_T, nq_pad, (unsigned long long *)qthr, uj, xord);
     return hip_status();
 }
 
@@ -1339,12 +1394,12 @@ extern "C" int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, 
                                     size_t q_base, int nq, const void *cblk, size_t c_rows_pad,
                                     size_t c_base, int nc, int n, const double *meta, int nsplit,
                                     double *part_d, int *part_i, double *part_T, int nq_pad,
-                                    double *qthr, int xord, void *stream)
+                                    double *qthr, int flags, void *stream)
 {
 #define CALL(T, KL, KP)                                                                        \
     return launch_dist_topk<T, KL, KP>((const T *)qblk, q_rows_pad, q_base, nq, (const T *)cblk, \
                                        c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i,  \
-                                       part_T, nq_pad, qthr, k, xord, (hipStream_t)stream)
+                                       part_T, nq_pad, qthr, k, flags, (hipStream_t)stream)
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
 }

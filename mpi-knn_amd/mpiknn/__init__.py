@@ -42,6 +42,7 @@ API_SYMBOLS = (
     "knn_ctx_rescan_step", "knn_ctx_rescan_end", "knn_search_packed", "knn_ctx_info",
     "knn_ctx_profile", "knn_block_bytes_dt", "knn_block_meta_offset_dt", "knn_block_pack_dt",
     "knn_ctx_create_dt", "knn_classify_device", "knn_search_mpi_compat",
+    "knn_ctx_contraction_bits",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -99,6 +100,7 @@ def _load():
         "knn_ctx_rescan_end": ([p, p, p], i),
         "knn_search_packed": ([p, p, sz, p, p], i),
         "knn_ctx_info": ([p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], i),
+        "knn_ctx_contraction_bits": ([p], i),
         "knn_ctx_profile": ([p, i, ctypes.POINTER(d), ctypes.POINTER(d), ctypes.POINTER(i)], i),
     }
     for name, (args, res) in sig.items():
@@ -295,3 +297,7 @@ class Context:
         mode, splits = ctypes.c_int(), ctypes.c_int()
         _check(lib.knn_ctx_info(self._h, ctypes.byref(mode), ctypes.byref(splits)), "knn_ctx_info")
         return mode.value, splits.value
+
+    def contraction_bits(self):
+        """64 / 32, or 16 when this fp32 search contracts on fp16 MFMA."""
+        return lib.knn_ctx_contraction_bits(self._h)

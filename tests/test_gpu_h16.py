@@ -1,0 +1,64 @@
+"""fp16-MFMA contraction of fp32 searches (include/knn.h
+knn_ctx_contraction_bits): taken exactly when every value is an integer
+with max|x| <= 2048 inside the fp32 exact-integer range, and then
+bit-identical to the oracle (the fp32 path's contract on integer data).
+Checked through bench's per-rank engine (mpiknn.ring.GpuEngine) so the
+contraction actually used is visible."""
+import numpy as np
+import pytest
+
+import datasets
+
+pytestmark = pytest.mark.gpu
+
+
+def run_engine(X, k):
+    import torch
+    import mpiknn.ring as ring
+    m, n = X.shape
+    eng = ring.GpuEngine(torch, 0, n, m, m, k, dtype="f32")
+    eng.pack(torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to("cuda:0"),
+             layout_col=False)
+    ring.ring_search(None, torch, eng, 0, 1, m, 0)
+    return eng.result(), eng.ctx.contraction_bits()
+
+
+def check(oracle, X, k, bits):
+    got, b = run_engine(X, k)
+    assert b == bits
+    ref = oracle.knn(X.astype(np.float32).astype(np.float64), k)
+    assert np.array_equal(got["idx"], ref["idx"])
+    assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64))
+
+
+def test_h16_sift_like(oracle):
+    check(oracle, datasets.sift_like(20000, 128), 32, 16)
+
+
+def test_h16_boundary_values(oracle):
+    # max|x| = 2048 and n max^2 = 2^23 exactly: the largest eligible data
+    rng = np.random.default_rng(3)
+    X = rng.integers(0, 2049, (4000, 2)).astype(np.float64)
+    X[:50, 0] = 2048.0
+    X[100] = X[7]                                  # exact duplicate
+    check(oracle, X, 16, 16)
+
+
+def test_h16_signed_with_duplicates(oracle):
+    rng = np.random.default_rng(4)
+    X = rng.integers(-60, 61, (3000, 100)).astype(np.float64)
+    X[200:260] = X[0]                              # a mass of duplicates
+    check(oracle, X, 16, 16)
+    check(oracle, X, 100, 16)                      # the k=33..128 variant
+
+
+def test_h16_not_taken_above_2048(oracle):
+    rng = np.random.default_rng(5)
+    X = rng.integers(0, 2050, (3000, 1)).astype(np.float64)
+    X[0, 0] = 2049.0
+    check(oracle, X, 8, 32)
+
+
+def test_h16_not_taken_real_valued(oracle):
+    X = datasets.digits_real()[0]
+    check(oracle, X, 30, 32)
