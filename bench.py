@@ -201,6 +201,10 @@ def main():
         "unit": "TFLOP/s",
         "mfma_input": {64: "f64", 32: "f32", 16: "f16 (exact on this data)"}[cbits],
         "frac": (achieved / peak) if achieved else None,
+        # the same achieved rate against the MFMA peak of the path's own
+        # element type (BASELINE's "% of fp64 MFMA peak" for mnist)
+        "frac_of_dtype_peak": (achieved / (FP64_MFMA_PEAK_TFLOPS if dtype == "f64"
+                                           else FP32_MFMA_PEAK_TFLOPS)) if achieved else None,
         "traffic": traffic,
         # distance-stage busy time (union of the overlapped k_dist_topk
         # launches, knn_ctx_profile) per launch; at P = 1 one launch a step

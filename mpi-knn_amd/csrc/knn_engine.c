@@ -313,7 +313,7 @@ int knn_ctx_destroy(knn_ctx_t *c)
 int knn_ctx_contraction_bits(const knn_ctx_t *c)
 {
     if (!c) return 0;
-    return c->dtype == KNN_F64 ? 64 : (c->h16 ? 16 : 32);
+    return c->h16 ? 16 : (c->dtype == KNN_F64 ? 64 : 32);
 }
 
 int knn_ctx_info(const knn_ctx_t *c, int *mode, int *splits)
@@ -328,8 +328,16 @@ int knn_ctx_info(const knn_ctx_t *c, int *mode, int *splits)
  * n range^2 <= 2^24) with max|x| <= 2048, so every value is exact in fp16:
  * the fp16 MFMA contraction gives the fp32 path's dot products bit for bit
  * (knn_kernels.hip, knn_to_h8). */
-static int knn_h16_exact(const double *meta, size_t n)
+static int knn_h16_exact(const double *meta, size_t n, int dtype)
 {
+    if (dtype == KNN_F64) {
+        /* fp64 INT mode (knn_mode<double>) with max|x| <= 256: fp16 inputs
+         * exact, fp32 sums exact over 256 features (knn_to_h4) */
+        if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e290)) return 0;
+        const double mx = meta[KNN_META_MAXABS];
+        return meta[KNN_META_NONINT] == 0.0 && mx <= 256.0 &&
+               mx * mx <= 2251799813685248.0 / (4.0 * (double)n);
+    }
     if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e37)) return 0;
     const double mx = meta[KNN_META_MAXABS];
     const double rg = meta[KNN_META_MAXPOS] + meta[KNN_META_MAXNEG];
@@ -350,7 +358,7 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
     c->nstep = 0;
     c->nfail = 0;
     c->h16 = 0;
-    if (c->dtype == KNN_F32) {
+    {
         /* one 64-byte read of the reduced meta per search picks the
          * contraction: fp16 MFMA when it is exact (knn_h16_exact) */
         const char *off = getenv("KNN_NO_H16");
@@ -358,7 +366,7 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
             double hm[KNN_META_DOUBLES];
             HIPCHK(hipMemcpyAsync(hm, d_meta, sizeof(hm), hipMemcpyDeviceToHost, (hipStream_t)stream));
             HIPCHK(hipStreamSynchronize((hipStream_t)stream));
-            c->h16 = knn_h16_exact(hm, c->n);
+            c->h16 = knn_h16_exact(hm, c->n, c->dtype);
         }
     }
     HIPCHK(hipMemsetAsync(c->fail_count, 0, sizeof(int), (hipStream_t)stream));

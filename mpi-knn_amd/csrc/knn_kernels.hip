@@ -70,6 +70,28 @@ template <typename T> static constexpr int knn_bk() { return 128 / (int)sizeof(T
 // 4g..4g+3 of pieces 0 and 1) into one 8-half operand; the query side is
 // converted identically, so each chunk's 32 features are summed once.
 typedef _Float16 knn_h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 knn_h4 __attribute__((ext_vector_type(4)));
+// fp64 blocks (H16 with ES 8): integer data with max|x| <= 256.  A chunk is
+// 16 features; lane (row, g) converts its two 16-byte slots (features
+// 2g, 2g+1 of pieces 0 and 1) into one 4-half operand of
+// v_mfma_f32_16x16x16_f16.  Its fp32 sums are exact over 16 chunks (256
+// features: |partial| <= 256 * 2^16 = 2^24), then flushed into the fp64
+// accumulators, so the tile's dot products are the fp64 path's, bit for bit.
+// Hardware conversions only: a plain (_Float16)(double) cast is folded
+// into one f64->f16 rounding, which hipcc emulates in ~30 integer
+// instructions (measured 2.5x slower than the fp64 kernel).  Here
+// v_cvt_f32_f64 then v_cvt_pkrtz_f16_f32 -- exact for these integers.
+typedef __fp16 knn_hp2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ knn_h4 knn_to_h4(dbl2 a, dbl2 b)
+{
+    const knn_hp2 lo = __builtin_amdgcn_cvt_pkrtz((float)a.x, (float)a.y);
+    const knn_hp2 hi = __builtin_amdgcn_cvt_pkrtz((float)b.x, (float)b.y);
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    u2 w;
+    w.x = __builtin_bit_cast(unsigned int, lo);
+    w.y = __builtin_bit_cast(unsigned int, hi);
+    return __builtin_bit_cast(knn_h4, w);
+}
 __device__ __forceinline__ knn_h8 knn_to_h8(flt4 a, flt4 b)
 {
     knn_h8 r;
@@ -382,6 +404,10 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
 {
     constexpr int NST = KNN_NST;
     constexpr int BK = knn_bk<T>();                   // features per 128-B chunk
+    // fp64 H16 (knn_to_h4): the fp32 MFMA output layout, row 4g + r of a
+    // 16-row m-tile in lane group g, register r, instead of fp64's g + 4r
+    constexpr bool H16D = H16 != 0 && sizeof(T) == 8;
+    auto rowmap = [](int gg, int r) { return H16D ? 4 * gg + r : KT<T>::row(gg, r); };
     constexpr int ES = (int)sizeof(T);
     typedef typename KT<T>::acc_t acc_t;
     typedef typename KT<T>::frag_t frag_t;
@@ -452,6 +478,22 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     acc_t acc[8];
 #pragma unroll
     for (int mt = 0; mt < 8; mt++) acc[mt] = (acc_t){0, 0, 0, 0};
+    // fp64 H16: fp32 partial sums of up to 16 chunks (see knn_to_h4)
+    flt4 acc32[H16D ? 8 : 1];
+#pragma unroll
+    for (int mt = 0; mt < (H16D ? 8 : 1); mt++) acc32[mt] = (flt4){0, 0, 0, 0};
+    int grp = 0;
+    auto flush32 = [&]() {
+        if constexpr (H16D) {
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) acc[mt][r] += (double)acc32[H16D ? mt : 0][r];
+                acc32[H16D ? mt : 0] = (flt4){0, 0, 0, 0};
+            }
+            grp = 0;
+        }
+    };
 
     LDS_AS char *lds = (LDS_AS char *)smem;
 
@@ -466,7 +508,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const int cn_unit = (__builtin_amdgcn_readfirstlane(wave) & (NU / 64 - 1)) * 64 + lane;
     const int cn_p = ES == 8 ? cn_unit >> 1 : cn_unit;       // norm index g*32 + k
     const int cn_k = cn_p & 31;
-    const int cn_src_off = (16 * (cn_k >> 2) + KT<T>::row(cn_p >> 5, cn_k & 3)) * ES +
+    const int cn_src_off = (16 * (cn_k >> 2) + rowmap(cn_p >> 5, cn_k & 3)) * ES +
                            (ES == 8 ? (cn_unit & 1) * 4 : 0);
     int s_c = 0, s_t = t_lo, s_fc = 0;                       // chunk being staged
     // Every wave stages its own m-tile and its own 16 queries.  All staging
@@ -580,7 +622,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 for (int mt = 0; mt < 8; mt++)
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
-                        const int row = row0 + 16 * mt + KT<T>::row(g, r);
+                        const int row = row0 + 16 * mt + rowmap(g, r);
                         if (!(row < nc && (long)c_base + row != gq)) pend_all &= ~(1u << (4 * mt + r));
                     }
             }
@@ -601,7 +643,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 const T w2 = b2 ? v[5] : v[4], w3 = b2 ? v[7] : v[6];
                 const T x0 = b3 ? w1 : w0, x1 = b3 ? w3 : w2;
                 const T dd = pend_all ? (b4 ? x1 : x0) : (T)KNN_INF;
-                const int ii = (int)(c_base + row0 + 16 * (b >> 2) + KT<T>::row(g, b & 3));
+                const int ii = (int)(c_base + row0 + 16 * (b >> 2) + rowmap(g, b & 3));
                 pend_all &= pend_all - 1;
                 list_insert<KL>(L, I, dd, ii);
                 if constexpr (EPI == 3) {
@@ -700,7 +742,30 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             gnorm(t + 2, t + 2);
             for (int fc = 0; fc < nfc; fc++, c++) {
                 LDS_AS char *cs = cs_of(c);
-                if constexpr (H16 != 0) {
+                if constexpr (H16D) {
+                    // fp16 MFMA on converted fp64 fragments (knn_to_h4); the
+                    // output is in the fp32 layout (rowmap)
+                    glds1(1);
+                    glds1(2);
+                    glds1(3);
+                    const knn_h4 bh = knn_to_h4(rdq(cs, 0), rdq(cs, 1));
+#pragma unroll
+                    for (int mt = 0; mt < 8; mt++) {
+                        const frag_t a0 = *(const LDS_AS frag_t *)(cs + mt * 2048 + fslot);
+                        const frag_t a1 = *(const LDS_AS frag_t *)(cs + mt * 2048 + fslot1);
+                        acc32[H16D ? mt : 0] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+                            knn_to_h4(a0, a1), bh, acc32[H16D ? mt : 0], 0, 0, 0);
+                    }
+                    if (++grp == 16) flush32();
+                    advance();
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    if constexpr (SELF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    glds1(0);
+                    continue;
+                }
+                if constexpr (H16 != 0 && ES == 4) {
                     // fp16 MFMA on converted fp32 fragments (knn_to_h8): one
                     // 16x16x32 per m-tile per chunk.  Same staging sequence
                     // as below: loads 1..3 of chunk c+3, the chunk barrier,
@@ -753,6 +818,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 // S3: (p1, mt4-7) on f1 || read (p0, mt0-3) of chunk c+1
                 segment(f1, b1, 1, [&](int j) { rd(cs1, 0, 0, f0, j); }, [&]() { glds1(0); });
             }
+            flush32();
             epilogue(t, acc);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // no LDS-DMA left in flight
@@ -1365,8 +1431,8 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     const T *cnorm = cblk + c_rows_pad * np;
     const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
     const dim3 grid((unsigned)(nqb_grid * nsplit));
-    if constexpr (sizeof(T) == 4) {
-        if (flags & KNN_DIST_H16) {   // host-checked: INT mode and max|x| <= 2048
+    {
+        if (flags & KNN_DIST_H16) {   // host-checked: INT mode and max|x| <= 2048 (fp64: 256)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 0, 1>), grid, dim3(512), 0, s,
                                qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles, nsplit,
                                nqb, meta, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr,

@@ -1,7 +1,9 @@
-"""fp16-MFMA contraction of fp32 searches (include/knn.h
-knn_ctx_contraction_bits): taken exactly when every value is an integer
-with max|x| <= 2048 inside the fp32 exact-integer range, and then
-bit-identical to the oracle (the fp32 path's contract on integer data).
+"""fp16-MFMA contraction (include/knn.h knn_ctx_contraction_bits): fp32
+searches take it when every value is an integer with max|x| <= 2048 inside
+the fp32 exact-integer range, fp64 searches when every value is an integer
+with max|x| <= 256 (fp32 partial sums over 256 features stay exact, then
+fp64 accumulation).  Either way the result must be bit-identical to the
+oracle.
 Checked through bench's per-rank engine (mpiknn.ring.GpuEngine) so the
 contraction actually used is visible."""
 import numpy as np
@@ -12,21 +14,22 @@ import datasets
 pytestmark = pytest.mark.gpu
 
 
-def run_engine(X, k):
+def run_engine(X, k, dtype="f32"):
     import torch
     import mpiknn.ring as ring
     m, n = X.shape
-    eng = ring.GpuEngine(torch, 0, n, m, m, k, dtype="f32")
-    eng.pack(torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to("cuda:0"),
+    eng = ring.GpuEngine(torch, 0, n, m, m, k, dtype=dtype)
+    npdt = np.float32 if dtype == "f32" else np.float64
+    eng.pack(torch.from_numpy(np.ascontiguousarray(X, dtype=npdt)).to("cuda:0"),
              layout_col=False)
     ring.ring_search(None, torch, eng, 0, 1, m, 0)
     return eng.result(), eng.ctx.contraction_bits()
 
 
-def check(oracle, X, k, bits):
-    got, b = run_engine(X, k)
+def check(oracle, X, k, bits, dtype="f32"):
+    got, b = run_engine(X, k, dtype)
     assert b == bits
-    ref = oracle.knn(X.astype(np.float32).astype(np.float64), k)
+    ref = oracle.knn(X.astype(np.float32).astype(np.float64) if dtype == "f32" else X, k)
     assert np.array_equal(got["idx"], ref["idx"])
     assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64))
 
@@ -62,3 +65,26 @@ def test_h16_not_taken_above_2048(oracle):
 def test_h16_not_taken_real_valued(oracle):
     X = datasets.digits_real()[0]
     check(oracle, X, 30, 32)
+
+
+def test_h16_fp64_mnist_like(oracle):
+    check(oracle, datasets.mnist_like(3000, 784, seed=21)[0], 30, 16, "f64")
+
+
+def test_h16_fp64_signed_boundary(oracle):
+    # |x| = 256 with 784 features: every 256-feature fp32 partial sum may
+    # reach 2^24 exactly -- the largest eligible data
+    rng = np.random.default_rng(8)
+    X = rng.integers(-256, 257, (2500, 784)).astype(np.float64)
+    X[:20] = 256.0
+    X[20:40] = -256.0
+    X[41] = X[40]
+    check(oracle, X, 32, 16, "f64")
+
+
+def test_h16_fp64_not_taken(oracle):
+    rng = np.random.default_rng(9)
+    X = rng.integers(0, 258, (2000, 50)).astype(np.float64)
+    X[0, 0] = 257.0
+    check(oracle, X, 30, 64, "f64")
+    check(oracle, datasets.digits_real()[0], 30, 64, "f64")
