@@ -176,6 +176,18 @@ KNN_API size_t knn_block_meta_offset(size_t cap, size_t n);
 KNN_API size_t knn_block_bytes_dt(size_t cap, size_t n, int dtype);
 KNN_API size_t knn_block_meta_offset_dt(size_t cap, size_t n, int dtype);
 
+/* Ring wire form of a packed block: the elements as int16, norms and meta
+ * verbatim -- a quarter (fp64) or half (fp32) of the block bytes on the
+ * link.  Exact only when knn_wire_ok(host copy of the reduced meta): every
+ * value an integer with max|x| <= 32767.  knn_wire_unpack restores the
+ * block bit for bit.  Used by mpiknn/ring.py between RCCL hops. */
+KNN_API size_t knn_wire_bytes(size_t cap, size_t n, int dtype);
+KNN_API int knn_wire_ok(const double *h_meta);
+KNN_API int knn_wire_pack(void *d_wire, const void *d_block, size_t cap, size_t n, int dtype,
+                          void *stream);
+KNN_API int knn_wire_unpack(void *d_block, const void *d_wire, size_t cap, size_t n, int dtype,
+                            void *stream);
+
 /* Pack rows (<= cap) points from a device source.  layout KNN_COLMAJOR:
  * element (i, j) at d_src[i + j*ld] (ld >= rows; the .mat layout,
  * serial:82); KNN_ROWMAJOR: d_src[i*ld + j] (ld >= n; blk:81-109).

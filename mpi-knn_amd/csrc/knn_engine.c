@@ -118,6 +118,46 @@ size_t knn_block_bytes_dt(size_t cap, size_t n, int dtype)
 
 size_t knn_block_meta_offset(size_t cap, size_t n) { return knn_block_meta_offset_dt(cap, n, KNN_F64); }
 
+/* Wire form: [rows_pad x n_pad int16][the block's norms and meta, verbatim] */
+size_t knn_wire_bytes(size_t cap, size_t n, int dtype)
+{
+    if (!dtype_ok(dtype)) return 0;
+    const size_t rp = knn_rows_pad(cap), np = knn_n_pad_dt(n, dtype);
+    return knn_round_up(rp * np * sizeof(short) + rp * knn_esize(dtype) +
+                        KNN_META_DOUBLES * sizeof(double), 16);
+}
+
+int knn_wire_ok(const double *h_meta)
+{
+    if (!h_meta) return 0;
+    return h_meta[KNN_META_NONINT] == 0.0 && h_meta[KNN_META_NONFINITE] == 0.0 &&
+           h_meta[KNN_META_MAXABS] <= 32767.0;
+}
+
+static int wire_copy(void *dst, const void *src, size_t cap, size_t n, int dtype, int unpack,
+                     void *stream)
+{
+    if (!dst || !src || !dtype_ok(dtype)) return KNN_ERR_INVALID;
+    const size_t rp = knn_rows_pad(cap), np = knn_n_pad_dt(n, dtype), es = knn_esize(dtype);
+    const size_t cnt = rp * np;
+    const size_t tail = rp * es + KNN_META_DOUBLES * sizeof(double);
+    RCHK(knn_launch_wire(unpack, dst, src, dtype, cnt, stream));
+    char *d = (char *)dst + cnt * (unpack ? es : sizeof(short));
+    const char *s = (const char *)src + cnt * (unpack ? sizeof(short) : es);
+    HIPCHK(hipMemcpyAsync(d, s, tail, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return KNN_OK;
+}
+
+int knn_wire_pack(void *d_wire, const void *d_block, size_t cap, size_t n, int dtype, void *stream)
+{
+    return wire_copy(d_wire, d_block, cap, n, dtype, 0, stream);
+}
+
+int knn_wire_unpack(void *d_block, const void *d_wire, size_t cap, size_t n, int dtype, void *stream)
+{
+    return wire_copy(d_block, d_wire, cap, n, dtype, 1, stream);
+}
+
 size_t knn_block_bytes(size_t cap, size_t n) { return knn_block_bytes_dt(cap, n, KNN_F64); }
 
 int knn_block_pack_dt(void *d_block, int dtype, size_t cap, size_t rows, size_t n,

@@ -94,11 +94,13 @@ int knn_launch_rescan_end(int kp, const int *fail_list, int nfail, const double 
 int knn_launch_vote(knn_neighbour_t *nb, size_t m, int k, int nclasses, int rule,
                     const double *labels, size_t nlabels, size_t q_base, int *pred,
                     unsigned long long *matches, void *stream);
+/* knn_kernels.hip: block elements <-> int16 wire elements (cnt % 8 == 0) */
+int knn_launch_wire(int unpack, void *dst, const void *src, int dtype, size_t cnt, void *stream);
+/* knn_engine.c: the value knn_last_search_seconds() returns (this thread) */
+void knn_set_last_search_seconds(double s);
 
 #ifdef __cplusplus
 }
 #endif
-/* knn_engine.c: the value knn_last_search_seconds() returns (this thread) */
-void knn_set_last_search_seconds(double s);
 
 #endif

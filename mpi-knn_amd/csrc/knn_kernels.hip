@@ -1389,6 +1389,56 @@ static int launch_pack(T *blk, size_t cap, size_t rows, size_t n, const S *src, 
     return hip_status();
 }
 
+// Ring wire form of a packed block (knn_wire_pack / knn_wire_unpack): the
+// element array as int16 (exact for integer data with max|x| <= 32767),
+// 8 elements a thread; norms and meta travel verbatim (hipMemcpyAsync).
+typedef short knn_s8v __attribute__((ext_vector_type(8)));
+template <typename T>
+__global__ __launch_bounds__(256) void k_wire_pack(knn_s8v *__restrict__ w, const T *__restrict__ b,
+                                                   size_t n8)
+{
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+        knn_s8v v;
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] = (short)b[8 * i + e];
+        w[i] = v;
+    }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_wire_unpack(T *__restrict__ b, const knn_s8v *__restrict__ w,
+                                                     size_t n8)
+{
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+        const knn_s8v v = w[i];
+#pragma unroll
+        for (int e = 0; e < 8; e++) b[8 * i + e] = (T)v[e];
+    }
+}
+
+extern "C" int knn_launch_wire(int unpack, void *dst, const void *src, int dtype, size_t cnt,
+                               void *stream)
+{
+    if (cnt % 8) return KNN_ERR_INVALID;
+    const size_t n8 = cnt / 8;
+    const unsigned grid = (unsigned)(n8 / 256 + 1 < 4096 ? n8 / 256 + 1 : 4096);
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == KNN_F64 && !unpack)
+        hipLaunchKernelGGL(k_wire_pack<double>, dim3(grid), dim3(256), 0, s, (knn_s8v *)dst,
+                           (const double *)src, n8);
+    else if (dtype == KNN_F64)
+        hipLaunchKernelGGL(k_wire_unpack<double>, dim3(grid), dim3(256), 0, s, (double *)dst,
+                           (const knn_s8v *)src, n8);
+    else if (dtype == KNN_F32 && !unpack)
+        hipLaunchKernelGGL(k_wire_pack<float>, dim3(grid), dim3(256), 0, s, (knn_s8v *)dst,
+                           (const float *)src, n8);
+    else if (dtype == KNN_F32)
+        hipLaunchKernelGGL(k_wire_unpack<float>, dim3(grid), dim3(256), 0, s, (float *)dst,
+                           (const knn_s8v *)src, n8);
+    else
+        return KNN_ERR_INVALID;
+    return hip_status();
+}
+
 extern "C" int knn_launch_pack(void *blk, int dtype, size_t cap, size_t rows, size_t n,
                                const void *src, int src_dtype, size_t ld, int layout, void *stream)
 {

@@ -42,7 +42,8 @@ API_SYMBOLS = (
     "knn_ctx_rescan_step", "knn_ctx_rescan_end", "knn_search_packed", "knn_ctx_info",
     "knn_ctx_profile", "knn_block_bytes_dt", "knn_block_meta_offset_dt", "knn_block_pack_dt",
     "knn_ctx_create_dt", "knn_classify_device", "knn_search_mpi_compat",
-    "knn_ctx_contraction_bits",
+    "knn_ctx_contraction_bits", "knn_wire_bytes", "knn_wire_ok", "knn_wire_pack",
+    "knn_wire_unpack",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -101,6 +102,10 @@ def _load():
         "knn_search_packed": ([p, p, sz, p, p], i),
         "knn_ctx_info": ([p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], i),
         "knn_ctx_contraction_bits": ([p], i),
+        "knn_wire_bytes": ([sz, sz, i], sz),
+        "knn_wire_ok": ([p], i),
+        "knn_wire_pack": ([p, p, sz, sz, i, p], i),
+        "knn_wire_unpack": ([p, p, sz, sz, i, p], i),
         "knn_ctx_profile": ([p, i, ctypes.POINTER(d), ctypes.POINTER(d), ctypes.POINTER(i)], i),
     }
     for name, (args, res) in sig.items():
@@ -224,6 +229,25 @@ def block_bytes(cap, n, dtype="f64"):
 
 def block_meta_offset(cap, n, dtype="f64"):
     return lib.knn_block_meta_offset_dt(cap, n, DTYPES[dtype])
+
+
+def wire_bytes(cap, n, dtype="f64"):
+    return lib.knn_wire_bytes(cap, n, DTYPES[dtype])
+
+
+def wire_ok(meta_host):
+    """meta_host: the reduced block meta as a float64 numpy array."""
+    m = np.ascontiguousarray(meta_host, dtype=np.float64)
+    return bool(lib.knn_wire_ok(_ptr(m)))
+
+
+def wire_pack(d_wire, d_block, cap, n, dtype="f64", stream=0):
+    _check(lib.knn_wire_pack(d_wire, d_block, cap, n, DTYPES[dtype], stream or None), "knn_wire_pack")
+
+
+def wire_unpack(d_block, d_wire, cap, n, dtype="f64", stream=0):
+    _check(lib.knn_wire_unpack(d_block, d_wire, cap, n, DTYPES[dtype], stream or None),
+           "knn_wire_unpack")
 
 
 def block_pack(d_block, cap, rows, n, d_src, ld, layout, stream=0, dtype="f64", src_dtype="f64"):

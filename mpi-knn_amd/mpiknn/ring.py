@@ -16,7 +16,15 @@ mpi-knn-parallel_blocking.c:122-244 / _non_blocking.c:132-259:
   two: knn_ctx_step orders the caller's stream after step s - STEP_LAG only
   (its distance kernels overlap, include/knn.h), so the hop posted at step
   h may only land in the buffer step h - STEP_LAG - 1 read;
-* the block meta is combined with one all_reduce(MAX) of 8 doubles.
+* the block meta is combined with one all_reduce(MAX) of 8 doubles;
+* integer data (knn_wire_ok on the reduced meta: max|x| <= 32767) travels
+  in the int16 wire form -- a quarter of an fp64 block, half of an fp32
+  one -- and each rank unpacks what it receives (bit for bit) into an
+  element block for its kernels.  Two wire receive buffers alternate: the
+  one a hop lands in was last forwarded one hop earlier (r.wait()) and
+  unpacked before that, both ordered on the caller's stream.  At P = 8 an
+  fp64 MNIST block is 47 MB, about one contraction step on xGMI; its wire
+  form is 12 MB.  KNN_NO_WIRE=1 sends element blocks.
 
 The engine object does the per-block work (GpuEngine: libknn kernels on the
 current HIP stream).  Tests substitute a CPU engine to check the schedule
@@ -48,6 +56,7 @@ class GpuEngine:
         self.qb = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
         self.rx = tuple(torch.empty(nb, dtype=torch.uint8, device=self.dev)
                         for _ in range(mpiknn.STEP_LAG + 2))
+        self._wires = None
         self.meta_off = mpiknn.block_meta_offset(R, n, dtype)
         self.meta = torch.zeros(mpiknn.META_DOUBLES, dtype=torch.float64, device=self.dev)
         self.out = torch.zeros(max(nq, 1) * k * 16, dtype=torch.uint8, device=self.dev)
@@ -74,6 +83,22 @@ class GpuEngine:
         self.meta.copy_(self.qb[self.meta_off:self.meta_off + 8 * self.mk.META_DOUBLES]
                         .view(self.torch.float64))
 
+    def wires(self):
+        """own wire block + two wire receive buffers (allocated on first use)"""
+        if self._wires is None:
+            wb = self.mk.wire_bytes(self.R, self.n, self.dtype)
+            self._wires = tuple(self.torch.empty(wb, dtype=self.torch.uint8, device=self.dev)
+                                for _ in range(3))
+        return self._wires
+
+    def wire_pack(self, wire):
+        self.mk.wire_pack(wire.data_ptr(), self.qb.data_ptr(), self.R, self.n, self.dtype,
+                          self.stream())
+
+    def wire_unpack(self, buf, wire):
+        self.mk.wire_unpack(buf.data_ptr(), wire.data_ptr(), self.R, self.n, self.dtype,
+                            self.stream())
+
     def begin(self, q_base):
         self.ctx.begin(self.qb.data_ptr(), self.R, q_base, self.meta.data_ptr(), self.stream())
 
@@ -99,21 +124,32 @@ def ring_search(dist, torch, engine, rank, P, m, q_base):
     (engine.pack done).  Collective calls: all_reduce(meta), P-1 hops per
     pass, all_reduce(unresolved).  Returns the number of queries that took
     the exact rescan pass on this rank."""
+    import os
     R, blocks = partition(m, P)
+    wire = False
     if P > 1:
         dist.all_reduce(engine.meta, op=dist.ReduceOp.MAX)
+        wire = (os.environ.get("KNN_NO_WIRE", "0") != "1" and hasattr(engine, "wires") and
+                engine.mk.wire_ok(engine.meta.cpu().numpy()))
     engine.begin(q_base)
 
     rx = engine.rx
-    state = {"cur": engine.qb, "hop": 0}
+    # cur: the element block folded next; send: what goes on the link
+    state = {"cur": engine.qb, "send": engine.qb, "hop": 0}
+    if wire:
+        own_w, wa, wb = engine.wires()
+        engine.wire_pack(own_w)
+        state["send"] = own_w
 
     def one_pass(off, rescan):
         for s in range(P):
             reqs = []
             if s < P - 1:
-                nxt = rx[state["hop"] % len(rx)]
-                ops = [dist.P2POp(dist.isend, state["cur"], (rank + 1) % P),
-                       dist.P2POp(dist.irecv, nxt, (rank - 1) % P)]
+                h = state["hop"]
+                nxt = rx[h % len(rx)]
+                land = ((wa, wb)[h % 2]) if wire else nxt
+                ops = [dist.P2POp(dist.isend, state["send"], (rank + 1) % P),
+                       dist.P2POp(dist.irecv, land, (rank - 1) % P)]
                 reqs = dist.batch_isend_irecv(ops)
             b = (rank - off - s) % P
             base, rows = blocks[b]
@@ -121,7 +157,10 @@ def ring_search(dist, torch, engine, rank, P, m, q_base):
             for r in reqs:
                 r.wait()
             if s < P - 1:
+                if wire:
+                    engine.wire_unpack(nxt, land)
                 state["cur"] = nxt
+                state["send"] = land
                 state["hop"] += 1
 
     one_pass(0, False)

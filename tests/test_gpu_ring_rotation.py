@@ -23,9 +23,10 @@ class _Req:
         pass
 
 
-def loopback_dist(torch, rank, P, packed, metas):
+def loopback_dist(torch, rank, P, packed, metas, wires):
     """A torch.distributed stand-in for rank `rank` of a P-ring whose packed
-    blocks are `packed` (block b = rank b's own block)."""
+    blocks are `packed` (block b = rank b's own block) and whose wire forms
+    (mpiknn.wire_pack) are `wires`."""
     hop = {"n": 0}
     ns = types.SimpleNamespace()
     ns.ReduceOp = types.SimpleNamespace(MAX="max", SUM="sum")
@@ -47,7 +48,8 @@ def loopback_dist(torch, rank, P, packed, metas):
         for fn, buf, peer in ops:
             if fn is irecv:
                 # hop h brings the block that started on rank - h - 1
-                src = packed[(rank - hop["n"] - 1) % P]
+                b = (rank - hop["n"] - 1) % P
+                src = wires[b] if buf.numel() == wires[b].numel() else packed[b]
                 buf.copy_(src, non_blocking=True)
         hop["n"] += 1
         return [_Req()]
@@ -58,12 +60,14 @@ def loopback_dist(torch, rank, P, packed, metas):
 
 
 @pytest.mark.parametrize("P", [2, 4, 7])
-@pytest.mark.parametrize("kind", ["int", "real"])
-def test_ring_search_rotation(knn, P, kind):
+@pytest.mark.parametrize("kind", ["int", "real", "int-nowire"])
+def test_ring_search_rotation(knn, P, kind, monkeypatch):
     import torch
     import mpiknn.ring as ring
 
-    X = datasets.mnist_like(3000, 784, seed=5)[0] if kind == "int" else datasets.digits_real()[0]
+    if kind == "int-nowire":
+        monkeypatch.setenv("KNN_NO_WIRE", "1")
+    X = datasets.mnist_like(3000, 784, seed=5)[0] if kind != "real" else datasets.digits_real()[0]
     m, n = X.shape
     full, _ = knn.search(X, 30)
     dev = torch.device("cuda", 0)
@@ -77,11 +81,38 @@ def test_ring_search_rotation(knn, P, kind):
         engines.append(e)
     packed = [e.qb.clone() for e in engines]
     metas = torch.stack([e.meta for e in engines])
+    wires = []
+    for e in engines:
+        w = torch.empty(knn.wire_bytes(R, n), dtype=torch.uint8, device=dev)
+        knn.wire_pack(w.data_ptr(), e.qb.data_ptr(), R, n, "f64", e.stream())
+        wires.append(w)
     for g, e in enumerate(engines):
         base, rows = blocks[g]
-        d = loopback_dist(torch, g, P, packed, metas)
+        d = loopback_dist(torch, g, P, packed, metas, wires)
         ring.ring_search(d, torch, e, g, P, m, base)
         got = e.result()
         assert np.array_equal(got["idx"], full[base:base + rows]["idx"]), (P, g)
         assert np.array_equal(got["distance"].view(np.uint64),
                               full[base:base + rows]["distance"].view(np.uint64)), (P, g)
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_wire_round_trip(knn, dtype):
+    """int16 wire form: pack -> unpack restores the packed block byte for
+    byte on integer data (knn_wire_ok), including norms and meta."""
+    import torch
+    import mpiknn.ring as ring
+    rng = np.random.default_rng(6)
+    X = rng.integers(-32767, 32768, (1000, 37)).astype(np.float64)
+    m, n = X.shape
+    e = ring.GpuEngine(torch, 0, n, m, m, 8, dtype=dtype)
+    e.pack(torch.from_numpy(X if dtype == "f64" else X.astype(np.float32)).to("cuda:0"),
+           layout_col=False)
+    assert knn.wire_ok(e.meta.cpu().numpy())
+    w = torch.empty(knn.wire_bytes(m, n, dtype), dtype=torch.uint8, device="cuda:0")
+    back = torch.empty_like(e.qb)
+    knn.wire_pack(w.data_ptr(), e.qb.data_ptr(), m, n, dtype, e.stream())
+    knn.wire_unpack(back.data_ptr(), w.data_ptr(), m, n, dtype, e.stream())
+    assert torch.equal(back, e.qb)
+    X[0, 0] = 32768.0
+    assert not knn.wire_ok(np.array([32768.0, 0, 0, 0, 0, 0, 0, 0]))
