@@ -36,7 +36,10 @@ struct knn_ctx {
     int k;
     int kp, kl;         /* state capacity / per-lane list length serving k */
     int xord;           /* k_dist_topk workgroup order (0 split-major, 1 XCD-grouped) */
-    int h16;            /* this search's fp32 contraction runs on fp16 MFMA (exact) */
+    int h16;            /* this search's contraction runs on fp16 MFMA (exact) */
+    int shadow;         /* ... staging fp16 shadow rows (qsh, csh) */
+    void *qsh, *csh[KNN_PSETS];
+    size_t qsh_bytes, csh_bytes;
     int cus;
     /* per-step partial lists of k_dist_topk, KNN_PSETS sets used in turn
      * (step s+1's distance kernel runs while step s is merged), each
@@ -190,6 +193,8 @@ static void ctx_free_buffers(knn_ctx_t *c)
         if (c->ev_d[b]) hipEventDestroy(c->ev_d[b]);
     }
     if (c->ms) hipStreamDestroy(c->ms);
+    hipFree(c->qsh);
+    for (int b = 0; b < KNN_PSETS; b++) hipFree(c->csh[b]);
     if (c->ev_in) hipEventDestroy(c->ev_in);
     hipFree(c->qthr);
     hipFree(c->st_d);
@@ -409,6 +414,22 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
             c->h16 = knn_h16_exact(hm, c->n, c->dtype);
         }
     }
+    /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
+     * element fragments in the kernel instead) */
+    const char *nosh = getenv("KNN_NO_SHADOW");
+    c->shadow = c->h16 && !(nosh && nosh[0] == '1');
+    if (c->shadow) {
+        const size_t need = c->q_rows_pad * knn_round_up(c->n, 64) * 2;
+        if (need > c->qsh_bytes) {
+            HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+            hipFree(c->qsh);
+            c->qsh = NULL;
+            c->qsh_bytes = 0;
+            if (hipMalloc(&c->qsh, need) != hipSuccess) return KNN_ERR_NOMEM;
+            c->qsh_bytes = need;
+        }
+        RCHK(knn_launch_shadow(c->qsh, d_qblock, c->dtype, c->q_rows_pad, c->n, stream));
+    }
     HIPCHK(hipMemsetAsync(c->fail_count, 0, sizeof(int), (hipStream_t)stream));
     RCHK(knn_launch_fill_inf(c->qthr, (int)c->nq_pad, stream));
     return KNN_OK;
@@ -538,6 +559,15 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     HIPCHK(hipEventRecord(c->ev_in, cs));
     HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
     if (c->nstep >= KNN_PSETS) HIPCHK(hipStreamWaitEvent(ds, c->ev_m[set], 0));
+    if (c->shadow) {
+        const size_t need = knn_rows_pad(c->block_cap) * knn_round_up(c->n, 64) * 2;
+        if (!c->csh[set]) {
+            /* first use of this set (hipMalloc may synchronise the device) */
+            if (hipMalloc(&c->csh[set], need) != hipSuccess) return KNN_ERR_NOMEM;
+        }
+        c->csh_bytes = need;
+        RCHK(knn_launch_shadow(c->csh[set], d_cblock, c->dtype, knn_rows_pad(nc), c->n, ds));
+    }
     hipEvent_t *ev = NULL;
     if (c->prof_on && c->prof_pending < KNN_PROF_STEPS) {
         ev = &c->prof_ev[3 * c->prof_pending++];
@@ -546,7 +576,10 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
                               c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr,
-                              (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0), ds));
+                              c->qsh, c->csh[set],
+                              (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0) |
+                                  (c->shadow ? KNN_DIST_SHADOW : 0),
+                              ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
     HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));

@@ -69,10 +69,14 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
                          const void *cblk, size_t c_rows_pad, size_t c_base, int nc,
                          int n, const double *meta, int nsplit,
                          double *part_d, int *part_i, double *part_T, int nq_pad,
-                         double *qthr, int flags, void *stream);
+                         double *qthr, const void *qsh, const void *csh, int flags,
+                         void *stream);
 /* knn_launch_dist_topk flags */
-#define KNN_DIST_XORD 1  /* XCD-grouped workgroup order                         */
-#define KNN_DIST_H16  2  /* fp32 blocks: fp16 MFMA contraction (exact data only) */
+#define KNN_DIST_XORD   1  /* XCD-grouped workgroup order                        */
+#define KNN_DIST_H16    2  /* fp16 MFMA contraction (exact data only)             */
+#define KNN_DIST_SHADOW 4  /* with H16: stage the fp16 shadow rows qsh / csh      */
+/* fp16 shadow rows (round_up(n, 64) halves a row) of a packed block */
+int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
 int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *part_i,
                      const double *part_T, int nsplit, int nq, int nq_pad, int first_step,

@@ -403,7 +403,10 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     int nq_pad, unsigned long long *__restrict__ qthr, int uj, int xord)
 {
     constexpr int NST = KNN_NST;
-    constexpr int BK = knn_bk<T>();                   // features per 128-B chunk
+    // H16 2: qblk / cblk are fp16 shadow rows (k_shadow), n_pad their row
+    // length; the norms stay in the element blocks
+    constexpr int RS = H16 == 2 ? 2 : (int)sizeof(T);   // bytes per staged element
+    constexpr int BK = 128 / RS;                      // features per 128-B chunk
     // fp64 H16 (knn_to_h4): the fp32 MFMA output layout, row 4g + r of a
     // 16-row m-tile in lane group g, register r, instead of fp64's g + 4r
     constexpr bool H16D = H16 != 0 && sizeof(T) == 8;
@@ -522,16 +525,17 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     auto glds1 = [&](int i) {
         if constexpr ((ABL & 1) != 0) return;
         if (!loader) return;
-        const unsigned r8 = 8u * ES * (unsigned)n_pad;             // 8 rows, bytes
-        const size_t fo = (size_t)BK * s_fc;
-        const T *cb = cblk + (size_t)((ABL & 128) ? t_lo : s_t) * KNN_TC * n_pad + fo;
-        const T *qb0 = qblk + (size_t)((ABL & 64) ? 0 : qrow0) * n_pad + fo;
+        const unsigned r8 = 8u * RS * (unsigned)n_pad;             // 8 rows, bytes
+        const size_t fo = (size_t)128 * s_fc;                      // chunk offset, bytes
+        const char *cb = (const char *)cblk +
+                         (size_t)((ABL & 128) ? t_lo : s_t) * KNN_TC * n_pad * RS + fo;
+        const char *qb0 = (const char *)qblk + (size_t)((ABL & 64) ? 0 : qrow0) * n_pad * RS + fo;
 #pragma unroll
         for (int hw = 0; hw < (SELF ? 1 : 2); hw++) {
             const int ww = SELF ? wave_s : (wave_s & 3) + 4 * hw;
             const unsigned dst = (unsigned)(uintptr_t)lds + (unsigned)(s_c & (NST - 1)) * 32768u +
                                  (unsigned)ww * 2048u;
-            const unsigned vo = (unsigned)((16 * ww + lr) * n_pad * ES + seg_b);
+            const unsigned vo = (unsigned)((16 * ww + lr) * n_pad * RS + seg_b);
             if (i == 0) bglds16(knn_rsrc(cb), vo, dst);
             if (i == 1) bglds16(knn_rsrc(cb), vo + r8, dst + 1024);
             if (i == 2) bglds16(knn_rsrc(qb0), vo, dst + 16384);
@@ -742,7 +746,40 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             gnorm(t + 2, t + 2);
             for (int fc = 0; fc < nfc; fc++, c++) {
                 LDS_AS char *cs = cs_of(c);
-                if constexpr (H16D) {
+                if constexpr (H16 == 2) {
+                    // fp16 shadow rows: a 16-byte slot is a whole 8-half
+                    // operand, two v_mfma_f32_16x16x32_f16 per m-tile per
+                    // 64-feature chunk, no conversion.  fp64: fp32 partial
+                    // sums flushed every 4 chunks (256 features, knn_to_h4)
+                    glds1(1);
+                    glds1(2);
+                    glds1(3);
+                    const knn_h8 q0 = *(const LDS_AS knn_h8 *)(cs + 16384 + wave * 2048 + fslot);
+                    const knn_h8 q1 = *(const LDS_AS knn_h8 *)(cs + 16384 + wave * 2048 + fslot1);
+#pragma unroll
+                    for (int mt = 0; mt < 8; mt++) {
+                        const knn_h8 a0 = *(const LDS_AS knn_h8 *)(cs + mt * 2048 + fslot);
+                        const knn_h8 a1 = *(const LDS_AS knn_h8 *)(cs + mt * 2048 + fslot1);
+                        if constexpr (H16D) {
+                            acc32[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, q0, acc32[mt], 0, 0, 0);
+                            acc32[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, q1, acc32[mt], 0, 0, 0);
+                        } else {
+                            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, q0, acc[mt], 0, 0, 0);
+                            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, q1, acc[mt], 0, 0, 0);
+                        }
+                    }
+                    if constexpr (H16D) {
+                        if (++grp == 4) flush32();
+                    }
+                    advance();
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    if constexpr (SELF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    glds1(0);
+                    continue;
+                }
+                if constexpr (H16 == 1 && H16D) {
                     // fp16 MFMA on converted fp64 fragments (knn_to_h4); the
                     // output is in the fp32 layout (rowmap)
                     glds1(1);
@@ -765,7 +802,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                     glds1(0);
                     continue;
                 }
-                if constexpr (H16 != 0 && ES == 4) {
+                if constexpr (H16 == 1 && ES == 4) {
                     // fp16 MFMA on converted fp32 fragments (knn_to_h8): one
                     // 16x16x32 per m-tile per chunk.  Same staging sequence
                     // as below: loads 1..3 of chunk c+3, the chunk barrier,
@@ -1415,6 +1452,49 @@ __global__ __launch_bounds__(256) void k_wire_unpack(T *__restrict__ b, const kn
     }
 }
 
+// fp16 shadow rows of a packed block for the H16 == 2 contraction: rows
+// of round_up(n, 64) halves (zero padded), converted with v_cvt_pkrtz
+// (exact: shadows are only made for integer data with max|x| <= 2048).
+template <typename T>
+__global__ __launch_bounds__(256) void k_shadow(knn_h8 *__restrict__ dst, const T *__restrict__ src,
+                                                size_t rows, int n, int nps, int npd)
+{
+    const size_t per = (size_t)npd / 8, tot = rows * per;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < tot; i += (size_t)gridDim.x * 256) {
+        const size_t r = i / per;
+        const int c = (int)(i - r * per) * 8;
+        const T *row = src + r * (size_t)nps;
+        unsigned w[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int j = c + 2 * e;
+            const float x0 = j < n ? (float)row[j] : 0.f;
+            const float x1 = j + 1 < n ? (float)row[j + 1] : 0.f;
+            w[e] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(x0, x1));
+        }
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        dst[i] = __builtin_bit_cast(knn_h8, (u4){w[0], w[1], w[2], w[3]});
+    }
+}
+
+extern "C" int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,
+                                 void *stream)
+{
+    const int npd = (int)knn_round_up(n, 64), nps = (int)knn_n_pad_dt(n, dtype);
+    const size_t tot = rows_pad * (size_t)npd / 8;
+    const unsigned grid = (unsigned)(tot / 256 + 1 < 8192 ? tot / 256 + 1 : 8192);
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == KNN_F64)
+        hipLaunchKernelGGL(k_shadow<double>, dim3(grid), dim3(256), 0, s, (knn_h8 *)dst,
+                           (const double *)blk, rows_pad, (int)n, nps, npd);
+    else if (dtype == KNN_F32)
+        hipLaunchKernelGGL(k_shadow<float>, dim3(grid), dim3(256), 0, s, (knn_h8 *)dst,
+                           (const float *)blk, rows_pad, (int)n, nps, npd);
+    else
+        return KNN_ERR_INVALID;
+    return hip_status();
+}
+
 extern "C" int knn_launch_wire(int unpack, void *dst, const void *src, int dtype, size_t cnt,
                                void *stream)
 {
@@ -1458,7 +1538,8 @@ template <typename T, int KL, int KP>
 static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int nq, const T *cblk,
                             size_t c_rows_pad, size_t c_base, int nc, int n, const double *meta,
                             int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
-                            double *qthr, int k, int flags, hipStream_t s)
+                            double *qthr, int k, const void *qsh, const void *csh, int flags,
+                            hipStream_t s)
 {
     const int xord = flags & 1;
     constexpr int dt = sizeof(T) == 8 ? KNN_F64 : KNN_F32;
@@ -1481,6 +1562,15 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     const T *cnorm = cblk + c_rows_pad * np;
     const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
     const dim3 grid((unsigned)(nqb_grid * nsplit));
+    if ((flags & KNN_DIST_SHADOW) && (flags & KNN_DIST_H16)) {
+        if (!qsh || !csh) return KNN_ERR_INVALID;
+        const int nps = (int)knn_round_up((size_t)n, 64);   // shadow row length (halves)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 0, 2>), grid, dim3(512), 0, s,
+                           (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
+                           nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
+                           (unsigned long long *)qthr, uj, xord);
+        return hip_status();
+    }
     {
         if (flags & KNN_DIST_H16) {   // host-checked: INT mode and max|x| <= 2048 (fp64: 256)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 0, 1>), grid, dim3(512), 0, s,
@@ -1510,12 +1600,14 @@ extern "C" int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, 
                                     size_t q_base, int nq, const void *cblk, size_t c_rows_pad,
                                     size_t c_base, int nc, int n, const double *meta, int nsplit,
                                     double *part_d, int *part_i, double *part_T, int nq_pad,
-                                    double *qthr, int flags, void *stream)
+                                    double *qthr, const void *qsh, const void *csh, int flags,
+                                    void *stream)
 {
 #define CALL(T, KL, KP)                                                                        \
     return launch_dist_topk<T, KL, KP>((const T *)qblk, q_rows_pad, q_base, nq, (const T *)cblk, \
                                        c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i,  \
-                                       part_T, nq_pad, qthr, k, flags, (hipStream_t)stream)
+                                       part_T, nq_pad, qthr, k, qsh, csh, flags,                  \
+                                       (hipStream_t)stream)
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
 }

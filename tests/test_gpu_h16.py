@@ -88,3 +88,12 @@ def test_h16_fp64_not_taken(oracle):
     X[0, 0] = 257.0
     check(oracle, X, 30, 64, "f64")
     check(oracle, datasets.digits_real()[0], 30, 64, "f64")
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_h16_fragment_conversion_path(oracle, monkeypatch, dtype):
+    """KNN_NO_SHADOW=1: the fp16 operands are converted from the element
+    fragments in the kernel instead of staged from fp16 shadow rows."""
+    monkeypatch.setenv("KNN_NO_SHADOW", "1")
+    X = datasets.mnist_like(2500, 784, seed=31)[0] if dtype == "f64" else datasets.sift_like(6000, 128)
+    check(oracle, X, 30, 16, dtype)
