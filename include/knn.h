@@ -188,6 +188,18 @@ KNN_API int knn_wire_pack(void *d_wire, const void *d_block, size_t cap, size_t 
 KNN_API int knn_wire_unpack(void *d_block, const void *d_wire, size_t cap, size_t n, int dtype,
                             void *stream);
 
+/* Shadow block of a packed block: its rows as fp16 (round_up(n, 64) halves
+ * a row), norms and meta verbatim.  When knn_ctx_shadow(ctx) is 1 after
+ * knn_ctx_begin (the fp16 contraction is exact for this search and staged
+ * from shadow rows), knn_ctx_step_shadow folds a shadow block instead of
+ * the element block -- the ring then moves shadow blocks (2 bytes an
+ * element).  The exact rescan (knn_ctx_rescan_step) still takes element
+ * blocks. */
+KNN_API size_t knn_shadow_bytes(size_t cap, size_t n, int dtype);
+KNN_API size_t knn_shadow_norm_offset(size_t cap, size_t n);
+KNN_API int knn_shadow_pack(void *d_sblock, const void *d_block, size_t cap, size_t n, int dtype,
+                            void *stream);
+
 /* Pack rows (<= cap) points from a device source.  layout KNN_COLMAJOR:
  * element (i, j) at d_src[i + j*ld] (ld >= rows; the .mat layout,
  * serial:82); KNN_ROWMAJOR: d_src[i*ld + j] (ld >= n; blk:81-109).
@@ -225,6 +237,11 @@ KNN_API int knn_ctx_begin(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap, si
  * later one: a ring rotates KNN_STEP_LAG + 2 receive buffers (knn_ring.c,
  * mpiknn/ring.py).  knn_ctx_end orders `stream` after every step. */
 #define KNN_STEP_LAG 2
+/* Shadow-block form of knn_ctx_step (knn_shadow_pack above); valid while
+ * knn_ctx_shadow(ctx) is 1 */
+KNN_API int knn_ctx_shadow(const knn_ctx_t *ctx);
+KNN_API int knn_ctx_step_shadow(knn_ctx_t *ctx, const void *d_sblock, size_t nc, size_t c_base,
+                                void *stream);
 KNN_API int knn_ctx_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
                  size_t c_base, void *stream);
 

@@ -161,6 +161,32 @@ int knn_wire_unpack(void *d_block, const void *d_wire, size_t cap, size_t n, int
     return wire_copy(d_block, d_wire, cap, n, dtype, 1, stream);
 }
 
+/* Shadow block: [rows_pad x round_up(n,64) fp16][the block's norms and
+ * meta, verbatim] -- what the fp16 contraction stages (knn_ctx_step_shadow) */
+size_t knn_shadow_norm_offset(size_t cap, size_t n)
+{
+    return knn_rows_pad(cap) * knn_round_up(n, 64) * 2;
+}
+
+size_t knn_shadow_bytes(size_t cap, size_t n, int dtype)
+{
+    if (!dtype_ok(dtype)) return 0;
+    return knn_round_up(knn_shadow_norm_offset(cap, n) + knn_rows_pad(cap) * knn_esize(dtype) +
+                        KNN_META_DOUBLES * sizeof(double), 16);
+}
+
+int knn_shadow_pack(void *d_sblock, const void *d_block, size_t cap, size_t n, int dtype, void *stream)
+{
+    if (!d_sblock || !d_block || !dtype_ok(dtype)) return KNN_ERR_INVALID;
+    const size_t rp = knn_rows_pad(cap);
+    RCHK(knn_launch_shadow(d_sblock, d_block, dtype, rp, n, stream));
+    const size_t tail = rp * knn_esize(dtype) + KNN_META_DOUBLES * sizeof(double);
+    HIPCHK(hipMemcpyAsync((char *)d_sblock + knn_shadow_norm_offset(cap, n),
+                          (const char *)d_block + rp * knn_n_pad_dt(n, dtype) * knn_esize(dtype),
+                          tail, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return KNN_OK;
+}
+
 size_t knn_block_bytes(size_t cap, size_t n) { return knn_block_bytes_dt(cap, n, KNN_F64); }
 
 int knn_block_pack_dt(void *d_block, int dtype, size_t cap, size_t rows, size_t n,
@@ -546,9 +572,13 @@ static int ensure_part_buffers(knn_ctx_t *c, int nsplit, int set)
  * enqueues after step s returns is ordered after step s-2 only, so a ring
  * rotates KNN_STEP_LAG + 2 receive buffers (knn.h).  knn_ctx_end joins
  * all. */
-int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, void *stream)
+/* d_sblock: a shadow block (knn_shadow_pack) used in place of d_cblock */
+static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sblock, size_t nc,
+                         size_t c_base, void *stream)
 {
-    if (!c || !d_cblock || nc == 0 || nc > c->block_cap) return KNN_ERR_INVALID;
+    if (!c || !(d_cblock || d_sblock) || nc == 0 || nc > c->block_cap) return KNN_ERR_INVALID;
+    if (d_sblock && !c->shadow) return KNN_ERR_INVALID;
+    if (!d_cblock) d_cblock = d_sblock;   /* INT mode: k_merge never reads its rows */
     HIPCHK(hipSetDevice(c->device));
     const int nsplit = choose_splits(c, nc);
     const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
@@ -559,7 +589,10 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     HIPCHK(hipEventRecord(c->ev_in, cs));
     HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
     if (c->nstep >= KNN_PSETS) HIPCHK(hipStreamWaitEvent(ds, c->ev_m[set], 0));
-    if (c->shadow) {
+    const void *csh = d_sblock, *cn_ptr = NULL;
+    if (d_sblock) {
+        cn_ptr = (const char *)d_sblock + knn_shadow_norm_offset(c->block_cap, c->n);
+    } else if (c->shadow) {
         const size_t need = knn_rows_pad(c->block_cap) * knn_round_up(c->n, 64) * 2;
         if (!c->csh[set]) {
             /* first use of this set (hipMalloc may synchronise the device) */
@@ -567,6 +600,7 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
         }
         c->csh_bytes = need;
         RCHK(knn_launch_shadow(c->csh[set], d_cblock, c->dtype, knn_rows_pad(nc), c->n, ds));
+        csh = c->csh[set];
     }
     hipEvent_t *ev = NULL;
     if (c->prof_on && c->prof_pending < KNN_PROF_STEPS) {
@@ -576,7 +610,7 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
                               knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
                               c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr,
-                              c->qsh, c->csh[set],
+                              c->qsh, csh, cn_ptr,
                               (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0) |
                                   (c->shadow ? KNN_DIST_SHADOW : 0),
                               ds));
@@ -595,6 +629,19 @@ int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, v
     c->nstep++;
     return KNN_OK;
 }
+
+int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, void *stream)
+{
+    return ctx_step_impl(c, d_cblock, NULL, nc, c_base, stream);
+}
+
+int knn_ctx_step_shadow(knn_ctx_t *c, const void *d_sblock, size_t nc, size_t c_base, void *stream)
+{
+    if (!d_sblock) return KNN_ERR_INVALID;
+    return ctx_step_impl(c, NULL, d_sblock, nc, c_base, stream);
+}
+
+int knn_ctx_shadow(const knn_ctx_t *c) { return c ? c->shadow : 0; }
 
 int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *stream)
 {

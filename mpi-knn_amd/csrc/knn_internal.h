@@ -69,8 +69,8 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
                          const void *cblk, size_t c_rows_pad, size_t c_base, int nc,
                          int n, const double *meta, int nsplit,
                          double *part_d, int *part_i, double *part_T, int nq_pad,
-                         double *qthr, const void *qsh, const void *csh, int flags,
-                         void *stream);
+                         double *qthr, const void *qsh, const void *csh, const void *cn_ptr,
+                         int flags, void *stream);
 /* knn_launch_dist_topk flags */
 #define KNN_DIST_XORD   1  /* XCD-grouped workgroup order                        */
 #define KNN_DIST_H16    2  /* fp16 MFMA contraction (exact data only)             */

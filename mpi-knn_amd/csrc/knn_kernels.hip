@@ -1538,8 +1538,8 @@ template <typename T, int KL, int KP>
 static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int nq, const T *cblk,
                             size_t c_rows_pad, size_t c_base, int nc, int n, const double *meta,
                             int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
-                            double *qthr, int k, const void *qsh, const void *csh, int flags,
-                            hipStream_t s)
+                            double *qthr, int k, const void *qsh, const void *csh,
+                            const void *cn_ptr, int flags, hipStream_t s)
 {
     const int xord = flags & 1;
     constexpr int dt = sizeof(T) == 8 ? KNN_F64 : KNN_F32;
@@ -1559,7 +1559,7 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
         nq_pad < nqb * KNN_TQ)
         return KNN_ERR_INVALID;
     const T *qnorm = qblk + q_rows_pad * np;
-    const T *cnorm = cblk + c_rows_pad * np;
+    const T *cnorm = cn_ptr ? (const T *)cn_ptr : cblk + c_rows_pad * np;
     const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
     const dim3 grid((unsigned)(nqb_grid * nsplit));
     if ((flags & KNN_DIST_SHADOW) && (flags & KNN_DIST_H16)) {
@@ -1600,13 +1600,13 @@ extern "C" int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, 
                                     size_t q_base, int nq, const void *cblk, size_t c_rows_pad,
                                     size_t c_base, int nc, int n, const double *meta, int nsplit,
                                     double *part_d, int *part_i, double *part_T, int nq_pad,
-                                    double *qthr, const void *qsh, const void *csh, int flags,
-                                    void *stream)
+                                    double *qthr, const void *qsh, const void *csh,
+                                    const void *cn_ptr, int flags, void *stream)
 {
 #define CALL(T, KL, KP)                                                                        \
     return launch_dist_topk<T, KL, KP>((const T *)qblk, q_rows_pad, q_base, nq, (const T *)cblk, \
                                        c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i,  \
-                                       part_T, nq_pad, qthr, k, qsh, csh, flags,                  \
+                                       part_T, nq_pad, qthr, k, qsh, csh, cn_ptr, flags,          \
                                        (hipStream_t)stream)
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL

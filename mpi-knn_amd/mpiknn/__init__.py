@@ -43,7 +43,8 @@ API_SYMBOLS = (
     "knn_ctx_profile", "knn_block_bytes_dt", "knn_block_meta_offset_dt", "knn_block_pack_dt",
     "knn_ctx_create_dt", "knn_classify_device", "knn_search_mpi_compat",
     "knn_ctx_contraction_bits", "knn_wire_bytes", "knn_wire_ok", "knn_wire_pack",
-    "knn_wire_unpack",
+    "knn_wire_unpack", "knn_shadow_bytes", "knn_shadow_norm_offset", "knn_shadow_pack",
+    "knn_ctx_shadow", "knn_ctx_step_shadow",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -106,6 +107,11 @@ def _load():
         "knn_wire_ok": ([p], i),
         "knn_wire_pack": ([p, p, sz, sz, i, p], i),
         "knn_wire_unpack": ([p, p, sz, sz, i, p], i),
+        "knn_shadow_bytes": ([sz, sz, i], sz),
+        "knn_shadow_norm_offset": ([sz, sz], sz),
+        "knn_shadow_pack": ([p, p, sz, sz, i, p], i),
+        "knn_ctx_shadow": ([p], i),
+        "knn_ctx_step_shadow": ([p, p, sz, sz, p], i),
         "knn_ctx_profile": ([p, i, ctypes.POINTER(d), ctypes.POINTER(d), ctypes.POINTER(i)], i),
     }
     for name, (args, res) in sig.items():
@@ -250,6 +256,15 @@ def wire_unpack(d_block, d_wire, cap, n, dtype="f64", stream=0):
            "knn_wire_unpack")
 
 
+def shadow_bytes(cap, n, dtype="f64"):
+    return lib.knn_shadow_bytes(cap, n, DTYPES[dtype])
+
+
+def shadow_pack(d_sblock, d_block, cap, n, dtype="f64", stream=0):
+    _check(lib.knn_shadow_pack(d_sblock, d_block, cap, n, DTYPES[dtype], stream or None),
+           "knn_shadow_pack")
+
+
 def block_pack(d_block, cap, rows, n, d_src, ld, layout, stream=0, dtype="f64", src_dtype="f64"):
     """knn_block_pack_dt on device pointers (ints).  layout COLMAJOR/ROWMAJOR;
     dtype = block element type, src_dtype = that of d_src."""
@@ -293,6 +308,14 @@ class Context:
 
     def step(self, d_cblock, nc, c_base, stream=0):
         _check(lib.knn_ctx_step(self._h, d_cblock, nc, c_base, stream or None), "knn_ctx_step")
+
+    def step_shadow(self, d_sblock, nc, c_base, stream=0):
+        _check(lib.knn_ctx_step_shadow(self._h, d_sblock, nc, c_base, stream or None),
+               "knn_ctx_step_shadow")
+
+    def shadow(self):
+        """1 while this search stages fp16 shadow rows (after begin)."""
+        return lib.knn_ctx_shadow(self._h)
 
     def end(self, d_out, stream=0):
         u = ctypes.c_size_t()

@@ -24,7 +24,12 @@ mpi-knn-parallel_blocking.c:122-244 / _non_blocking.c:132-259:
   one a hop lands in was last forwarded one hop earlier (r.wait()) and
   unpacked before that, both ordered on the caller's stream.  At P = 8 an
   fp64 MNIST block is 47 MB, about one contraction step on xGMI; its wire
-  form is 12 MB.  KNN_NO_WIRE=1 sends element blocks.
+  form is 12 MB.  KNN_NO_WIRE=1 sends element blocks;
+* when the search contracts on fp16 shadow rows (knn_ctx_shadow after
+  begin: exact-integer data), the ring moves shadow blocks instead --
+  2 bytes an element, folded with knn_ctx_step_shadow, no per-rank unpack
+  or conversion; the rare exact rescan then makes one more rotation of
+  element blocks.
 
 The engine object does the per-block work (GpuEngine: libknn kernels on the
 current HIP stream).  Tests substitute a CPU engine to check the schedule
@@ -102,6 +107,18 @@ class GpuEngine:
     def begin(self, q_base):
         self.ctx.begin(self.qb.data_ptr(), self.R, q_base, self.meta.data_ptr(), self.stream())
 
+    def shadow_block(self):
+        """own shadow block (knn_shadow_pack of the packed own block)"""
+        sb = self.mk.shadow_bytes(self.R, self.n, self.dtype)
+        if getattr(self, "_sqb", None) is None or self._sqb.numel() != sb:
+            self._sqb = self.torch.empty(sb, dtype=self.torch.uint8, device=self.dev)
+        self.mk.shadow_pack(self._sqb.data_ptr(), self.qb.data_ptr(), self.R, self.n, self.dtype,
+                            self.stream())
+        return self._sqb
+
+    def step_shadow(self, sbuf, rows, base):
+        self.ctx.step_shadow(sbuf.data_ptr(), rows, base, self.stream())
+
     def step(self, buf, rows, base, rescan=False):
         if rescan:
             self.ctx.rescan_step(buf.data_ptr(), rows, base, self.stream())
@@ -132,32 +149,45 @@ def ring_search(dist, torch, engine, rank, P, m, q_base):
         wire = (os.environ.get("KNN_NO_WIRE", "0") != "1" and hasattr(engine, "wires") and
                 engine.mk.wire_ok(engine.meta.cpu().numpy()))
     engine.begin(q_base)
+    shadow = (P > 1 and hasattr(engine, "step_shadow") and engine.ctx.shadow() == 1 and
+              os.environ.get("KNN_NO_SHADOW_RING", "0") != "1")
 
     rx = engine.rx
-    # cur: the element block folded next; send: what goes on the link
+    # cur: the block folded next; send: what goes on the link
     state = {"cur": engine.qb, "send": engine.qb, "hop": 0}
+    if shadow:
+        sb = engine.mk.shadow_bytes(engine.R, engine.n, engine.dtype)
+        own_s = engine.shadow_block()
+        srx = tuple(b[:sb] for b in rx)      # shadow blocks fit the element buffers
+        state["cur"] = state["send"] = own_s
     if wire:
         own_w, wa, wb = engine.wires()
+    if wire and not shadow:
         engine.wire_pack(own_w)
         state["send"] = own_w
 
     def one_pass(off, rescan):
+        use_shadow = shadow and not rescan
+        use_wire = wire and not use_shadow
         for s in range(P):
             reqs = []
             if s < P - 1:
                 h = state["hop"]
-                nxt = rx[h % len(rx)]
-                land = ((wa, wb)[h % 2]) if wire else nxt
+                nxt = (srx if use_shadow else rx)[h % len(rx)]
+                land = ((wa, wb)[h % 2]) if use_wire else nxt
                 ops = [dist.P2POp(dist.isend, state["send"], (rank + 1) % P),
                        dist.P2POp(dist.irecv, land, (rank - 1) % P)]
                 reqs = dist.batch_isend_irecv(ops)
             b = (rank - off - s) % P
             base, rows = blocks[b]
-            engine.step(state["cur"], rows, base, rescan)
+            if use_shadow:
+                engine.step_shadow(state["cur"], rows, base)
+            else:
+                engine.step(state["cur"], rows, base, rescan)
             for r in reqs:
                 r.wait()
             if s < P - 1:
-                if wire:
+                if use_wire:
                     engine.wire_unpack(nxt, land)
                 state["cur"] = nxt
                 state["send"] = land
@@ -171,6 +201,14 @@ def ring_search(dist, torch, engine, rank, P, m, q_base):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         total = int(t.item())
     if total > 0:
-        one_pass(P - 1, True)
+        if shadow:
+            # the rescan needs element rows: a fresh rotation from the own block
+            state.update(cur=engine.qb, send=engine.qb)
+            if wire:
+                engine.wire_pack(own_w)
+                state["send"] = own_w
+            one_pass(0, True)
+        else:
+            one_pass(P - 1, True)
         engine.rescan_end()
     return unresolved

@@ -23,10 +23,11 @@ class _Req:
         pass
 
 
-def loopback_dist(torch, rank, P, packed, metas, wires):
+def loopback_dist(torch, rank, P, packed, metas, wires, shadows):
     """A torch.distributed stand-in for rank `rank` of a P-ring whose packed
-    blocks are `packed` (block b = rank b's own block) and whose wire forms
-    (mpiknn.wire_pack) are `wires`."""
+    blocks are `packed` (block b = rank b's own block), with wire forms
+    (mpiknn.wire_pack) `wires` and shadow blocks (mpiknn.shadow_pack)
+    `shadows`; an irecv gets the form whose size it asks for."""
     hop = {"n": 0}
     ns = types.SimpleNamespace()
     ns.ReduceOp = types.SimpleNamespace(MAX="max", SUM="sum")
@@ -49,7 +50,8 @@ def loopback_dist(torch, rank, P, packed, metas, wires):
             if fn is irecv:
                 # hop h brings the block that started on rank - h - 1
                 b = (rank - hop["n"] - 1) % P
-                src = wires[b] if buf.numel() == wires[b].numel() else packed[b]
+                forms = {t[b].numel(): t[b] for t in (packed, wires, shadows)}
+                src = forms[buf.numel()]
                 buf.copy_(src, non_blocking=True)
         hop["n"] += 1
         return [_Req()]
@@ -60,13 +62,16 @@ def loopback_dist(torch, rank, P, packed, metas, wires):
 
 
 @pytest.mark.parametrize("P", [2, 4, 7])
-@pytest.mark.parametrize("kind", ["int", "real", "int-nowire"])
+@pytest.mark.parametrize("kind", ["int", "real", "int-nowire", "int-noshadow"])
 def test_ring_search_rotation(knn, P, kind, monkeypatch):
     import torch
     import mpiknn.ring as ring
 
     if kind == "int-nowire":
         monkeypatch.setenv("KNN_NO_WIRE", "1")
+        monkeypatch.setenv("KNN_NO_SHADOW_RING", "1")
+    if kind == "int-noshadow":
+        monkeypatch.setenv("KNN_NO_SHADOW_RING", "1")
     X = datasets.mnist_like(3000, 784, seed=5)[0] if kind != "real" else datasets.digits_real()[0]
     m, n = X.shape
     full, _ = knn.search(X, 30)
@@ -86,9 +91,14 @@ def test_ring_search_rotation(knn, P, kind, monkeypatch):
         w = torch.empty(knn.wire_bytes(R, n), dtype=torch.uint8, device=dev)
         knn.wire_pack(w.data_ptr(), e.qb.data_ptr(), R, n, "f64", e.stream())
         wires.append(w)
+    shadows = []
+    for e in engines:
+        sb = torch.empty(knn.shadow_bytes(R, n), dtype=torch.uint8, device=dev)
+        knn.shadow_pack(sb.data_ptr(), e.qb.data_ptr(), R, n, "f64", e.stream())
+        shadows.append(sb)
     for g, e in enumerate(engines):
         base, rows = blocks[g]
-        d = loopback_dist(torch, g, P, packed, metas, wires)
+        d = loopback_dist(torch, g, P, packed, metas, wires, shadows)
         ring.ring_search(d, torch, e, g, P, m, base)
         got = e.result()
         assert np.array_equal(got["idx"], full[base:base + rows]["idx"]), (P, g)

@@ -54,10 +54,27 @@ def main():
             mb = t[eng.meta_off:eng.meta_off + 8 * mpiknn.META_DOUBLES].view(torch.float64)
             eng.meta.copy_(torch.maximum(eng.meta, mb))   # the ring's all_reduce(MAX)
 
+        # what the ring moves: shadow blocks when the search stages fp16
+        # shadow rows (mpiknn/ring.py), element blocks otherwise
+        eng.begin(0)
+        shadow = P > 1 and eng.ctx.shadow() == 1
+        for b, (base, rows) in enumerate(blocks):
+            eng.step(bufs[b], rows, base)
+        eng.end()
+        sbufs = []
+        if shadow:
+            for t in bufs:
+                sb = torch.empty(mpiknn.shadow_bytes(R, n), dtype=torch.uint8, device=dev)
+                mpiknn.shadow_pack(sb.data_ptr(), t.data_ptr(), R, n, "f64", eng.stream())
+                sbufs.append(sb)
+
         def one():
             eng.begin(0)
             for b, (base, rows) in enumerate(blocks):
-                eng.step(bufs[b], rows, base)
+                if shadow:
+                    eng.step_shadow(sbufs[b], rows, base)
+                else:
+                    eng.step(bufs[b], rows, base)
             return eng.end()
 
         one()
@@ -73,8 +90,8 @@ def main():
         res[P] = {"rank_ms": dt * 1e3, "dist_busy_ms_per_pass": dist_ms / args.steps,
                   "dist_tflops": flops / (dist_ms * 1e-3) / 1e12 if dist_ms > 0 else None,
                   "exposed_merge_ms_per_pass": merge_ms / args.steps,
-                  "splits": eng.ctx.info()[1]}
-        del bufs, eng
+                  "splits": eng.ctx.info()[1], "shadow_ring": shadow}
+        del bufs, sbufs, eng
         torch.cuda.empty_cache()
     t1 = res[min(res)]["rank_ms"]
     for P, r in res.items():
