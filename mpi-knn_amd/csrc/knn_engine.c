@@ -44,10 +44,22 @@ struct knn_ctx {
     /* per-step partial lists of k_dist_topk, KNN_PSETS sets used in turn
      * (step s+1's distance kernel runs while step s is merged), each
      * grown to the largest split count used so far with it (part_splits) */
-    int part_splits[KNN_PSETS];
-    double *part_d[KNN_PSETS];
+    int part_splits[KNN_PSETS];       /* unused; kept for layout */
+    double *part_d[KNN_PSETS];        /* set pointers into the pair buffers */
     int *part_i[KNN_PSETS];
     double *part_T[KNN_PSETS];
+    /* sets 2j and 2j+1 share one allocation, the odd set right behind the
+     * even one, so a k_merge can read both steps' lists as one array */
+    double *pp_d[KNN_PSETS / 2];
+    int *pp_i[KNN_PSETS / 2];
+    double *pp_T[KNN_PSETS / 2];
+    int pp_cap[KNN_PSETS / 2];        /* splits per pair allocation */
+    /* an even step whose merge waits for the next step (pairing) */
+    int pend, pend_set, pend_nsplit, pend_nc, merged;
+    int even_nsplit;                  /* splits of the last even step: the odd set's offset */
+    const void *pend_cblk;
+    size_t pend_cbase;
+    hipEvent_t *pend_ev;
     /* overlapped step schedule (knn_ctx_step): distance kernels alternate
      * over two streams, merges run in order on a third */
     hipStream_t ds[2], ms;
@@ -208,11 +220,12 @@ int knn_block_pack(void *d_block, size_t cap, size_t rows, size_t n, const doubl
 
 static void ctx_free_buffers(knn_ctx_t *c)
 {
-    for (int b = 0; b < KNN_PSETS; b++) {
-        hipFree(c->part_d[b]);
-        hipFree(c->part_i[b]);
-        hipFree(c->part_T[b]);
+    for (int b = 0; b < KNN_PSETS; b++)
         if (c->ev_m[b]) hipEventDestroy(c->ev_m[b]);
+    for (int b = 0; b < KNN_PSETS / 2; b++) {
+        hipFree(c->pp_d[b]);
+        hipFree(c->pp_i[b]);
+        hipFree(c->pp_T[b]);
     }
     for (int b = 0; b < 2; b++) {
         if (c->ds[b]) hipStreamDestroy(c->ds[b]);
@@ -427,6 +440,10 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
     c->meta = d_meta;
     c->first_step = 1;
     c->nstep = 0;
+    c->pend = 0;
+    c->pend_nsplit = 0;
+    c->even_nsplit = 0;
+    c->merged = 0;
     c->nfail = 0;
     c->h16 = 0;
     {
@@ -536,24 +553,63 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     return best;
 }
 
-static int ensure_part_buffers(knn_ctx_t *c, int nsplit, int set)
+/* Partial lists of set `set` for nsplit splits.  Even set: the pair
+ * allocation grows to 2*nsplit splits (room for an odd step of the same
+ * size behind it).  Odd set: right behind the even set's `off` splits,
+ * growing the allocation only when nothing in it is pending. */
+static int ensure_part_buffers(knn_ctx_t *c, int nsplit, int set, int off)
 {
-    if (nsplit <= c->part_splits[set]) return KNN_OK;
-    /* the set may still be read by an earlier step's merge */
-    HIPCHK(hipStreamSynchronize(c->ms));
-    hipFree(c->part_d[set]);
-    hipFree(c->part_i[set]);
-    hipFree(c->part_T[set]);
-    c->part_d[set] = NULL;
-    c->part_i[set] = NULL;
-    c->part_T[set] = NULL;
-    c->part_splits[set] = 0;
-    const size_t npart = (size_t)nsplit * c->nq_pad * 4 * (size_t)c->kl;
-    if (hipMalloc((void **)&c->part_d[set], npart * sizeof(double)) != hipSuccess ||
-        hipMalloc((void **)&c->part_i[set], npart * sizeof(int)) != hipSuccess ||
-        hipMalloc((void **)&c->part_T[set], (size_t)nsplit * c->nq_pad * sizeof(double)) != hipSuccess)
-        return KNN_ERR_NOMEM;
-    c->part_splits[set] = nsplit;
+    const int pr = set >> 1;
+    const int need = (set & 1) ? off + nsplit : 2 * nsplit;
+    const size_t per = c->nq_pad * 4 * (size_t)c->kl;
+    if (need > c->pp_cap[pr]) {
+        if ((set & 1) && c->pend) return KNN_ERR_INVALID;   /* caller merges first */
+        /* the pair may still be read by an earlier step's merge */
+        HIPCHK(hipStreamSynchronize(c->ms));
+        hipFree(c->pp_d[pr]);
+        hipFree(c->pp_i[pr]);
+        hipFree(c->pp_T[pr]);
+        c->pp_d[pr] = NULL;
+        c->pp_i[pr] = NULL;
+        c->pp_T[pr] = NULL;
+        c->pp_cap[pr] = 0;
+        const int cap = need > 2 * nsplit ? need : 2 * nsplit;
+        if (hipMalloc((void **)&c->pp_d[pr], (size_t)cap * per * sizeof(double)) != hipSuccess ||
+            hipMalloc((void **)&c->pp_i[pr], (size_t)cap * per * sizeof(int)) != hipSuccess ||
+            hipMalloc((void **)&c->pp_T[pr], (size_t)cap * c->nq_pad * sizeof(double)) != hipSuccess)
+            return KNN_ERR_NOMEM;
+        c->pp_cap[pr] = cap;
+    }
+    const int o = (set & 1) ? off : 0;
+    c->part_d[set] = c->pp_d[pr] + (size_t)o * per;
+    c->part_i[set] = c->pp_i[pr] + (size_t)o * per;
+    c->part_T[set] = c->pp_T[pr] + (size_t)o * c->nq_pad;
+    return KNN_OK;
+}
+
+/* k_merge of `nsets` consecutive steps' lists (1, or 2 = a pending even
+ * step and the odd step behind it) starting at set `set`, on ms after
+ * their distance kernels; records ev_m of every covered set. */
+static int launch_merge_sets(knn_ctx_t *c, int set, int nsets, int nsplit_total, const void *cblk,
+                             size_t c_base, size_t nc)
+{
+    RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
+                          nsplit_total, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x,
+                          c->st_i, c->st_T, c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n,
+                          c->meta, c->ms));
+    c->merged = 1;
+    for (int x = 0; x < nsets; x++) HIPCHK(hipEventRecord(c->ev_m[(set + x) % KNN_PSETS], c->ms));
+    return KNN_OK;
+}
+
+/* merge the pending even step by itself */
+static int merge_pending(knn_ctx_t *c)
+{
+    if (!c->pend) return KNN_OK;
+    c->pend = 0;
+    RCHK(launch_merge_sets(c, c->pend_set, 1, c->pend_nsplit, c->pend_cblk, c->pend_cbase,
+                           (size_t)c->pend_nc));
+    if (c->pend_ev) HIPCHK(hipEventRecord(c->pend_ev[2], c->ms));
     return KNN_OK;
 }
 
@@ -583,7 +639,28 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     const int nsplit = choose_splits(c, nc);
     const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
     c->nsplit_last = nsplit;
-    RCHK(ensure_part_buffers(c, nsplit, set));
+    /* pairing: in exact-integer (fp16) searches two consecutive steps share
+     * one k_merge (8*nsplit + 1 <= 64 lists; INT mode never reads the
+     * block rows in k_merge) -- half the merges, which at P = 8 cost about
+     * as much as the contraction.  KNN_NO_PAIR=1 disables it. */
+    const char *np_env = getenv("KNN_NO_PAIR");
+    const int can_pair = c->h16 && nsplit <= 7 && !(np_env && np_env[0] == '1');
+    int pairing = 0;
+    if ((set & 1) && c->pend) {
+        pairing = can_pair && nsplit == c->pend_nsplit;
+        if (!pairing) RCHK(merge_pending(c));
+    }
+    {
+        if (!(set & 1)) c->even_nsplit = nsplit;
+        const int rc0 = ensure_part_buffers(c, nsplit, set, c->even_nsplit);
+        if (rc0 == KNN_ERR_INVALID && c->pend) {
+            RCHK(merge_pending(c));
+            pairing = 0;
+            RCHK(ensure_part_buffers(c, nsplit, set, c->even_nsplit));
+        } else if (rc0) {
+            return rc0;
+        }
+    }
     const void *cblk = d_cblock;
     hipStream_t cs = (hipStream_t)stream, ds = c->ds[ds_i];
     HIPCHK(hipEventRecord(c->ev_in, cs));
@@ -618,11 +695,27 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_in, 0));
-    RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set], nsplit,
-                          (int)c->nq, (int)c->nq_pad, c->first_step, c->st_d, c->st_x, c->st_i, c->st_T,
-                          c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n, c->meta, c->ms));
-    if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
-    HIPCHK(hipEventRecord(c->ev_m[set], c->ms));
+    if (pairing) {
+        /* the pending even step's kernel signalled ev_d[ds_i ^ 1], not yet
+         * re-recorded (the next record is step s+1's) */
+        HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i ^ 1], 0));
+        c->pend = 0;
+        RCHK(launch_merge_sets(c, c->pend_set, 2, 2 * nsplit, cblk, c_base, nc));
+        if (c->pend_ev) HIPCHK(hipEventRecord(c->pend_ev[2], c->ms));
+        if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
+    } else if (!(set & 1) && can_pair) {
+        c->pend = 1;
+        c->pend_set = set;
+        c->pend_nsplit = nsplit;
+        c->pend_cblk = cblk;
+        c->pend_cbase = c_base;
+        c->pend_nc = (int)nc;
+        c->pend_ev = ev;
+    } else {
+        RCHK(launch_merge_sets(c, set, 1, nsplit, cblk, c_base, nc));
+        if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
+    }
+    /* step s - 2 is merged by now (a pending step is always s itself) */
     if (c->nstep >= KNN_STEP_LAG)
         HIPCHK(hipStreamWaitEvent(cs, c->ev_m[(c->nstep - KNN_STEP_LAG) % KNN_PSETS], 0));
     c->first_step = 0;
@@ -648,6 +741,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     if (!c || !d_out || c->first_step) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
+    RCHK(merge_pending(c));
     HIPCHK(hipStreamWaitEvent(s, c->ev_m[(c->nstep - 1) % KNN_PSETS], 0));   /* the last merge */
     RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
                              (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
