@@ -669,6 +669,8 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     const void *csh = d_sblock, *cn_ptr = NULL;
     if (d_sblock) {
         cn_ptr = (const char *)d_sblock + knn_shadow_norm_offset(c->block_cap, c->n);
+    } else if (c->shadow && d_cblock == c->qblk && knn_rows_pad(nc) <= c->q_rows_pad) {
+        csh = c->qsh;   /* the query block itself (P = 1): its shadow exists */
     } else if (c->shadow) {
         const size_t need = knn_rows_pad(c->block_cap) * knn_round_up(c->n, 64) * 2;
         if (!c->csh[set]) {
