@@ -757,13 +757,14 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     c->mode = host[1];
     if (unresolved) *unresolved = (size_t)c->nfail;
     if (c->nfail > 0) {
-        if ((size_t)c->nfail > c->rs_cap) {
+        const size_t need = (size_t)c->nfail * (1 + (size_t)knn_rescan_chunks(c->nfail));
+        if (need > c->rs_cap) {
             hipFree(c->rs_d);
             hipFree(c->rs_i);
             c->rs_d = NULL;
             c->rs_i = NULL;
             c->rs_cap = 0;
-            size_t cap = (size_t)c->nfail;
+            size_t cap = need;
             if (hipMalloc((void **)&c->rs_d, cap * c->kp * sizeof(double)) != hipSuccess ||
                 hipMalloc((void **)&c->rs_i, cap * c->kp * sizeof(int)) != hipSuccess)
                 return KNN_ERR_NOMEM;

@@ -55,6 +55,15 @@ static inline int knn_kl_for(int kp)
 {
     return kp == KNN_KP ? KNN_KL : kp == KNN_KP_M ? KNN_KL_M : KNN_KL_L;
 }
+/* Corpus chunks of one exact rescan launch (k_rescan_step's grid.y): enough
+ * that (nfail / 16) x C workgroups fill the chip, at most 32.  The rescan
+ * list buffers hold 1 + C list sets (the running one, then one per chunk). */
+static inline int knn_rescan_chunks(int nfail)
+{
+    const int wg = (nfail + 15) / 16;
+    int c = wg > 0 ? (1024 + wg - 1) / wg : 1;
+    return c > 32 ? 32 : (c < 1 ? 1 : c);
+}
 static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
 {

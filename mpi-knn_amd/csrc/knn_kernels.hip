@@ -1217,7 +1217,8 @@ template <typename TE, int KP>
 __global__ __launch_bounds__(256) void k_rescan_step(
     const int *__restrict__ fail_list, int nfail, const double *__restrict__ fbound,
     const TE *__restrict__ qblk, int n_pad_q, const TE *__restrict__ cblk, size_t c_base,
-    int nc, int n, int n_pad, int k, double *__restrict__ rs_d, int *__restrict__ rs_i)
+    int nc, int n, int n_pad, int k, const double *rs_bound, double *rs_d, int *rs_i,
+    int rows_per_chunk, size_t chunk_stride)
 {
 #pragma clang fp contract(off)
     constexpr int KT = 4, QW = 4;
@@ -1228,6 +1229,11 @@ __global__ __launch_bounds__(256) void k_rescan_step(
     const int slot0 = blockIdx.x * 16 + wave * QW;
     if (slot0 >= nfail) return;                       // wave-uniform
     const int nr = (n + V - 1) / V;                   // 16-byte pieces per row
+    // corpus chunk blockIdx.y: rows [row0, row1) into its own list set
+    const int row0 = blockIdx.y * rows_per_chunk;
+    const int row1 = min(nc, row0 + rows_per_chunk);
+    rs_d += blockIdx.y * chunk_stride;
+    rs_i += blockIdx.y * chunk_stride;
 
     const TE *qp[QW];
     double dcut[QW];
@@ -1239,7 +1245,7 @@ __global__ __launch_bounds__(256) void k_rescan_step(
         done[x] = slot[x] >= nfail;
         const int q = done[x] ? fail_list[slot0] : fail_list[slot[x]];
         qp[x] = qblk + (size_t)q * n_pad_q;
-        const double kth = rs_d[(size_t)(done[x] ? slot0 : slot[x]) * KP + (k - 1)];
+        const double kth = rs_bound[(size_t)(done[x] ? slot0 : slot[x]) * KP + (k - 1)];
         dcut[x] = fmin(fbound[q], kth);
     }
     // running list of each query: old (read) and new (written at the end)
@@ -1267,7 +1273,7 @@ __global__ __launch_bounds__(256) void k_rescan_step(
 #pragma unroll
             for (int e = 0; e < KT; e++) { L[x][e] = KNN_INF; I[x][e] = 0x7fffffff; }
         }
-        for (int row = lane; row < nc; row += 64) {
+        for (int row = row0 + lane; row < row1; row += 64) {
             const vec_t *cr = (const vec_t *)(cblk + (size_t)row * n_pad);
             double S[QW] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 2
@@ -1382,6 +1388,52 @@ __global__ void k_rescan_init(double *rs_d, int *rs_i, int count)
 {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) { rs_d[i] = KNN_INF; rs_i[i] = -1; }
+}
+
+// Chunked rescan, second half: per query, the running list (list 0) and the
+// C chunk lists (each already the exact top k of its rows, ordered by
+// (key, idx)) merge into the running list.  One wave per query; lane j
+// holds the head of list j; k argmin rounds.  Row ids are disjoint across
+// lists, so no entry appears twice.
+template <int KP>
+__global__ __launch_bounds__(256) void k_rescan_merge(int nfail, int k, int nchunk,
+                                                      double *__restrict__ rs_d,
+                                                      int *__restrict__ rs_i)
+{
+    constexpr int NS = (KP + 63) / 64;
+    const int lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (slot >= nfail) return;                        // wave-uniform
+    const size_t stride = (size_t)nfail * KP;
+    const bool live = lane <= nchunk;
+    const double *ld = rs_d + (size_t)lane * stride + (size_t)slot * KP;
+    const int *li = rs_i + (size_t)lane * stride + (size_t)slot * KP;
+    double nd[NS];
+    int ni[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) { nd[s] = KNN_INF; ni[s] = -1; }
+    int pos = 0;
+    for (int r = 0; r < k; r++) {
+        double hd = (live && pos < k) ? ld[pos] : KNN_INF;
+        int hi = (hd == KNN_INF) ? 0x7fffffff : li[pos];
+        const double md = hd;
+        const int mi = hi;
+        wave_argmin(hd, hi);
+        if (hd == KNN_INF) break;                     // every list exhausted
+#pragma unroll
+        for (int s = 0; s < NS; s++)
+            if (lane == (r & 63) && (r >> 6) == s) { nd[s] = hd; ni[s] = hi; }
+        if (md == hd && mi == hi) pos++;             // ids are unique: one winner
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // reads of list 0 before its rewrite
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const int r = lane + 64 * s;
+        if (r < KP) {
+            rs_d[(size_t)slot * KP + r] = nd[s];
+            rs_i[(size_t)slot * KP + r] = (nd[s] == KNN_INF) ? -1 : ni[s];
+        }
+    }
 }
 
 __global__ void k_rescan_end(const int *__restrict__ fail_list, int nfail, int KP,
@@ -1667,13 +1719,33 @@ extern "C" int knn_launch_rescan_step(int dtype, int kp, const int *fail_list, i
                                       int *rs_i, void *stream)
 {
     if (nfail <= 0) return KNN_OK;
-    if (k <= 0 || k > kp) return KNN_ERR_INVALID;
+    if (k <= 0 || k > kp || nc <= 0) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
     hipStream_t s = (hipStream_t)stream;
+    // Few uncertified queries give few workgroups (16 queries each): split
+    // the block's rows over C chunks too (knn_rescan_chunks; the caller
+    // sized rs_d/rs_i for 1 + C list sets), then merge the chunk lists.
+    int C = knn_rescan_chunks(nfail);
+    const int min_rows = 256;
+    if (C > (nc + min_rows - 1) / min_rows) C = (nc + min_rows - 1) / min_rows;
+    if (C < 1) C = 1;
+    const int rpc = (nc + C - 1) / C;
+    C = (nc + rpc - 1) / rpc;
+    const size_t stride = (size_t)nfail * kp;
+    if (C > 1) {
+        hipLaunchKernelGGL(k_rescan_init, dim3((unsigned)((C * stride + 255) / 256)), dim3(256), 0, s,
+                           rs_d + stride, rs_i + stride, (int)(C * stride));
+    }
+    double *ld = C > 1 ? rs_d + stride : rs_d;
+    int *li = C > 1 ? rs_i + stride : rs_i;
 #define CALL(T, KL, KP)                                                                          \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_step<T, KP>), dim3((unsigned)((nfail + 15) / 16)), \
-                       dim3(256), 0, s, fail_list, nfail, fbound, (const T *)qblk, np,            \
-                       (const T *)cblk, c_base, nc, n, np, k, rs_d, rs_i);                        \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_step<T, KP>),                                    \
+                       dim3((unsigned)((nfail + 15) / 16), (unsigned)C), dim3(256), 0, s,         \
+                       fail_list, nfail, fbound, (const T *)qblk, np, (const T *)cblk, c_base, nc, \
+                       n, np, k, rs_d, ld, li, rpc, C > 1 ? stride : 0);                          \
+    if (C > 1)                                                                                   \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rescan_merge<KP>), dim3((unsigned)((nfail + 3) / 4)), \
+                           dim3(256), 0, s, nfail, k, C, rs_d, rs_i);                            \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL

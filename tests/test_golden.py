@@ -103,3 +103,18 @@ def test_gpu_mnist_full_size_fixture(knn):
     d = nb["distance"]
     assert np.all(d[:, 1:] >= d[:, :-1]) and np.all(d > 0)
     assert not np.any(nb["idx"] == np.arange(1, 60001)[:, None])
+
+
+@pytest.mark.gpu
+def test_gpu_mnist_single_split_rescan(knn, monkeypatch):
+    """One corpus split (KNN_SPLITS=1) leaves ~0.7% of the MNIST-shaped
+    queries uncertified, so they take the exact rescan,
+    chunked over the corpus (k_rescan_step grid.y + k_rescan_merge).  The
+    result must be byte-identical to the default split count's."""
+    X, _ = datasets.mnist_like(60000)
+    base, _ = knn.search(X, 30)
+    monkeypatch.setenv("KNN_SPLITS", "1")
+    one, _ = knn.search(X, 30)
+    assert base.tobytes() == one.tobytes()
+    g = load("mnist_like_sample.npz")
+    check_mnist_rows(one[g["rows"]], g)
