@@ -393,7 +393,8 @@ __device__ __forceinline__ void glds4(const void *src, unsigned lds_dst)
 // apart, 6 / 7 stage every workgroup's queries from block 0 / the corpus
 // from the split's first tile (L2-resident; wrong results), 11 each
 // segment's load before its first MFMA pair, 13 waves 0..3 stage for all
-// eight.  libknn instantiates <.., 1, 0>.
+// eight.  libknn instantiates <.., 1, 0> (element rows) and <.., 1, 8192, 2>
+// (fp16 shadow rows, where bit 13 measured 2% faster).
 template <typename T, int KL, int KS, int EPI = 1, int ABL = 0, int H16 = 0>
 __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const T *__restrict__ qblk, const T *__restrict__ qnorm, size_t q_base, int nq,
@@ -1617,7 +1618,10 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     if ((flags & KNN_DIST_SHADOW) && (flags & KNN_DIST_H16)) {
         if (!qsh || !csh) return KNN_ERR_INVALID;
         const int nps = (int)knn_round_up((size_t)n, 64);   // shadow row length (halves)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 0, 2>), grid, dim3(512), 0, s,
+        // shadow rows: waves 0..3 stage for their SIMD partners too (ABL bit
+        // 13; tools/probe/kbench16: mnist 10.36 -> 10.09-10.15 ms, partial
+        // lists byte-identical)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 8192, 2>), grid, dim3(512), 0, s,
                            (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
                            nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
                            (unsigned long long *)qthr, uj, xord);
