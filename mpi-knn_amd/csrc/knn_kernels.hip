@@ -1621,10 +1621,18 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
         // shadow rows: waves 0..3 stage for their SIMD partners too (ABL bit
         // 13; tools/probe/kbench16: mnist 10.36 -> 10.09-10.15 ms, partial
         // lists byte-identical)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 8192, 2>), grid, dim3(512), 0, s,
-                           (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
-                           nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                           (unsigned long long *)qthr, uj, xord);
+        // (KNN_STAGE_ALL=1: every wave stages its own rows, the earlier form)
+        static const int stage_all = getenv("KNN_STAGE_ALL") && getenv("KNN_STAGE_ALL")[0] == '1';
+        if (stage_all)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 0, 2>), grid, dim3(512), 0, s,
+                               (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
+                               nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
+                               (unsigned long long *)qthr, uj, xord);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 8192, 2>), grid, dim3(512), 0, s,
+                               (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
+                               nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
+                               (unsigned long long *)qthr, uj, xord);
         return hip_status();
     }
     {
