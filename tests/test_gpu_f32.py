@@ -105,14 +105,17 @@ def test_f32_duplicates_and_ties(knn, oracle):
     assert_same(run_engine(B, 30)[0], oracle.knn(B, 30), "binary ties f32")
 
 
-def test_f32_nonfinite_scan(knn, oracle):
+@pytest.mark.parametrize("m,n,k", [(300, 20, 30), (2000, 24, 100)])
+def test_f32_nonfinite_scan(knn, oracle, m, n, k):
+    """SCAN mode: every query takes the exact rescan, chunked over the
+    corpus rows (2000 rows: 8 chunks; k = 100 merges 128-slot lists)."""
     rng = np.random.default_rng(3)
-    X = rng.normal(0, 1, (300, 20))
+    X = rng.normal(0, 1, (m, n))
     X[5, 3] = np.nan
     X[17, 0] = np.inf
-    got, mode, _ = run_engine(X, 30)
-    assert mode == 2
-    assert_same(got, oracle.knn(rounded(X), 30), "nan/inf f32")
+    got, mode, u = run_engine(X, k)
+    assert mode == 2 and u == m
+    assert_same(got, oracle.knn(rounded(X), k), "nan/inf f32 k=%d" % k)
 
 
 @pytest.mark.parametrize("what,k", [("gist_like", 100), ("sift_like", 64), ("gaussian", 128),
