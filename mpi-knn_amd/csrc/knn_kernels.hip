@@ -621,7 +621,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             for (int mt = 0; mt < 8; mt++)
 #pragma unroll
                 for (int r = 0; r < 4; r++)
-                    pend_all |= (A[mt][r] <= lim && A[mt][r] > zfloor) ? (1u << (4 * mt + r)) : 0u;
+                    pend_all |= (A[mt][r] <= lim) ? (1u << (4 * mt + r)) : 0u;
             if (masked) {
 #pragma unroll
                 for (int mt = 0; mt < 8; mt++)
@@ -647,7 +647,10 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 const T w0 = b2 ? v[1] : v[0], w1 = b2 ? v[3] : v[2];
                 const T w2 = b2 ? v[5] : v[4], w3 = b2 ? v[7] : v[6];
                 const T x0 = b3 ? w1 : w0, x1 = b3 ? w3 : w2;
-                const T dd = pend_all ? (b4 ? x1 : x0) : (T)KNN_INF;
+                // d^2 <= zfloor (INT mode: an exact duplicate, S == 0) is
+                // dropped here rather than in the survivor mask (rare)
+                const T dsel = b4 ? x1 : x0;
+                const T dd = (pend_all && dsel > zfloor) ? dsel : (T)KNN_INF;
                 const int ii = (int)(c_base + row0 + 16 * (b >> 2) + rowmap(g, b & 3));
                 pend_all &= pend_all - 1;
                 list_insert<KL>(L, I, dd, ii);
@@ -1618,11 +1621,13 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     if ((flags & KNN_DIST_SHADOW) && (flags & KNN_DIST_H16)) {
         if (!qsh || !csh) return KNN_ERR_INVALID;
         const int nps = (int)knn_round_up((size_t)n, 64);   // shadow row length (halves)
-        // shadow rows: waves 0..3 stage for their SIMD partners too (ABL bit
-        // 13; tools/probe/kbench16: mnist 10.36 -> 10.09-10.15 ms, partial
-        // lists byte-identical)
-        // (KNN_STAGE_ALL=1: every wave stages its own rows, the earlier form)
-        static const int stage_all = getenv("KNN_STAGE_ALL") && getenv("KNN_STAGE_ALL")[0] == '1';
+        // shadow rows: waves 0..3 may stage for their SIMD partners too (ABL
+        // bit 13; partial lists byte-identical, tools/probe/kbench16)
+        // Every wave stages its own rows (ABL 0) for fp64 blocks (mnist 10.0
+        // vs 10.1 ms); fp32 (sift) 607 vs 691 ms with waves 0..3 staging.
+        // KNN_STAGE_ALL=0/1 overrides.
+        static const char *sa_env = getenv("KNN_STAGE_ALL");
+        const int stage_all = sa_env ? sa_env[0] == '1' : (int)(sizeof(T) == 8);
         if (stage_all)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 0, 2>), grid, dim3(512), 0, s,
                                (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
