@@ -35,6 +35,9 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-knn_amd"))
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix (spec; 78.2 measured, tools/probe)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix (spec, MI355X_MICROARCH.md; 155 measured)
 FP16_MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 matrix (spec ~2.5 PF, MI355X_MICROARCH.md)
+I8_MFMA_PEAK_TOPS = 5000.0      # dense int8 matrix: 2x the fp16 rate per clock (MI355X_MICROARCH.md)
+
+METRIC = "all-kNN queries/sec (MNIST-784, k=30) at 1/2/4/8 GPUs + % MFMA peak"   # BASELINE.json
 
 WORKLOADS = {
     # name: (m, n, k, dtype, layout_col, description)
@@ -192,14 +195,15 @@ def main():
     # the MFMA the contraction ran on: fp32 searches on exactly representable
     # 8-bit-style integer data contract on fp16 MFMA (include/knn.h)
     peak = {64: FP64_MFMA_PEAK_TFLOPS, 32: FP32_MFMA_PEAK_TFLOPS,
-            16: FP16_MFMA_PEAK_TFLOPS}[cbits]
+            16: FP16_MFMA_PEAK_TFLOPS, 8: I8_MFMA_PEAK_TOPS}[cbits]
     roofline = {
         "kernel": "k_dist_topk",
         "bound": "mfma",
         "achieved": achieved,
         "peak": peak,
         "unit": "TFLOP/s",
-        "mfma_input": {64: "f64", 32: "f32", 16: "f16 (exact on this data)"}[cbits],
+        "mfma_input": {64: "f64", 32: "f32", 16: "f16 (exact on this data)",
+                       8: "i8 (exact on this data: int32 dot products)"}[cbits],
         "frac": (achieved / peak) if achieved else None,
         # the same achieved rate against the MFMA peak of the path's own
         # element type (BASELINE's "% of fp64 MFMA peak" for mnist)
@@ -213,7 +217,9 @@ def main():
         "exposed_merge_ms_per_step": merge_ms / max(args.steps, 1),
     }
     out = {
-        "metric": "all-kNN queries/sec (MNIST-784, k=30) at 1/2/4/8 GPUs + % MFMA peak",
+        "metric": METRIC if args.workload == "mnist" else
+                  "all-kNN queries/sec (%s, k=%d) at %d GPUs + %% MFMA peak" % (
+                      wdesc.split(" k=")[0].replace("all-kNN ", ""), k, P),
         "value": m / (ms_per_step * 1e-3),
         "unit": "queries/s",
         "n_gpus": P,

@@ -227,6 +227,11 @@ KNN_API int knn_ctx_destroy(knn_ctx_t *ctx);
  * max-reduced meta of every corpus block. */
 KNN_API int knn_ctx_begin(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap, size_t q_base,
                   const double *d_meta, void *stream);
+/* The same with the host copy of the reduced meta (h_meta, 8 doubles; the
+ * ring drivers hold it after their all-reduce), so begin does not read it
+ * back from the device (no stream synchronisation).  h_meta NULL = begin. */
+KNN_API int knn_ctx_begin_meta(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap, size_t q_base,
+                               const double *d_meta, const double *h_meta, void *stream);
 
 /* Fold one packed corpus block (nc rows, global ids c_base..) into the
  * running neighbour lists.  Blocks may come in any order (ring order).
@@ -237,9 +242,16 @@ KNN_API int knn_ctx_begin(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap, si
  * later one: a ring rotates KNN_STEP_LAG + 2 receive buffers (knn_ring.c,
  * mpiknn/ring.py).  knn_ctx_end orders `stream` after every step. */
 #define KNN_STEP_LAG 2
-/* Shadow-block form of knn_ctx_step (knn_shadow_pack above); valid while
- * knn_ctx_shadow(ctx) is 1 */
+/* Shadow-block form of knn_ctx_step; valid while knn_ctx_shadow(ctx) is
+ * nonzero after knn_ctx_begin: 1 = fp16 shadow blocks (knn_shadow_pack),
+ * 2 = byte blocks of the int8 contraction (8-bit-window integer data, n <=
+ * 896: rows as int8 x - o, o from the reduced meta, plus int32 norms).
+ * knn_ctx_shadow_bytes / knn_ctx_shadow_pack size and pack a block of
+ * capacity cap in the context's current form (the form a ring moves). */
 KNN_API int knn_ctx_shadow(const knn_ctx_t *ctx);
+KNN_API size_t knn_ctx_shadow_bytes(const knn_ctx_t *ctx, size_t cap);
+KNN_API int knn_ctx_shadow_pack(knn_ctx_t *ctx, void *d_sblock, const void *d_block, size_t cap,
+                                void *stream);
 KNN_API int knn_ctx_step_shadow(knn_ctx_t *ctx, const void *d_sblock, size_t nc, size_t c_base,
                                 void *stream);
 KNN_API int knn_ctx_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
@@ -266,10 +278,12 @@ KNN_API int knn_search_packed(knn_ctx_t *ctx, const void *d_block, size_t m,
 KNN_API int knn_ctx_info(const knn_ctx_t *ctx, int *mode, int *splits);
 
 /* Input width in bits of the MFMA contraction of the current search: 64
- * (fp64 blocks), 32 (fp32 blocks), or 16 when an fp32 search runs its
- * contraction on fp16 MFMA because that is exact for its data (integers
- * with max|x| <= 2048 in the fp32 exact-integer range; set by
- * knn_ctx_begin; KNN_NO_H16=1 disables it).  0 for a NULL context. */
+ * (fp64 blocks), 32 (fp32 blocks), 16 when it runs on fp16 MFMA because
+ * that is exact for the data (integers with max|x| <= 256 (fp64) / 2048
+ * (fp32) in the exact-integer range; KNN_NO_H16=1 disables it), or 8 when
+ * it runs on int8 MFMA (integers inside a window of 256 values, n <= 896:
+ * exact int32 dot products; KNN_NO_I8=1 disables it).  Set by
+ * knn_ctx_begin.  0 for a NULL context. */
 KNN_API int knn_ctx_contraction_bits(const knn_ctx_t *ctx);
 
 /* Kernel timing with HIP events on the launch streams (the timers of

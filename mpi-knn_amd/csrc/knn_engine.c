@@ -25,7 +25,7 @@
         if (rc_) return rc_;     \
     } while (0)
 
-#define KNN_MAX_SPLITS 15 /* merge kernel: 4*splits + 1 lists <= 64 lanes */
+#define KNN_MAX_LISTS 63  /* merge kernel: lpq*splits + 1 lists <= 64 lanes */
 #define KNN_PSETS 4       /* partial-list sets: step s uses set s % 4   */
 #define KNN_PROF_STEPS 64 /* steps timed between two knn_ctx_end calls */
 
@@ -37,14 +37,17 @@ struct knn_ctx {
     int kp, kl;         /* state capacity / per-lane list length serving k */
     int xord;           /* k_dist_topk workgroup order (0 split-major, 1 XCD-grouped) */
     int h16;            /* this search's contraction runs on fp16 MFMA (exact) */
-    int shadow;         /* ... staging fp16 shadow rows (qsh, csh) */
+    int i8;             /* ... on int8 MFMA over byte blocks (knn_i8.hip, exact) */
+    int shadow;         /* step_shadow form: 0 none, 1 fp16 shadow rows, 2 byte blocks */
     void *qsh, *csh[KNN_PSETS];
     size_t qsh_bytes, csh_bytes;
+    void *qs8, *cs8[KNN_PSETS];   /* byte blocks: the queries, converted corpus blocks */
+    size_t qs8_bytes;
+    int lpq, klx;       /* partial lists of the active kernel: lpq per query and split, klx long */
     int cus;
     /* per-step partial lists of k_dist_topk, KNN_PSETS sets used in turn
      * (step s+1's distance kernel runs while step s is merged), each
      * grown to the largest split count used so far with it (part_splits) */
-    int part_splits[KNN_PSETS];       /* unused; kept for layout */
     double *part_d[KNN_PSETS];        /* set pointers into the pair buffers */
     int *part_i[KNN_PSETS];
     double *part_T[KNN_PSETS];
@@ -54,6 +57,7 @@ struct knn_ctx {
     int *pp_i[KNN_PSETS / 2];
     double *pp_T[KNN_PSETS / 2];
     int pp_cap[KNN_PSETS / 2];        /* splits per pair allocation */
+    size_t pp_per[KNN_PSETS / 2];     /* list entries per split it was sized for */
     /* an even step whose merge waits for the next step (pairing) */
     int pend, pend_set, pend_nsplit, pend_nc, merged;
     int even_nsplit;                  /* splits of the last even step: the odd set's offset */
@@ -83,6 +87,7 @@ struct knn_ctx {
     int first_step;
     int nsplit_last;
     size_t split_nc;    /* choose_splits cache: corpus rows -> split count */
+    int split_lpq;
     int split_best;
     int nfail;
     int mode;
@@ -234,6 +239,8 @@ static void ctx_free_buffers(knn_ctx_t *c)
     if (c->ms) hipStreamDestroy(c->ms);
     hipFree(c->qsh);
     for (int b = 0; b < KNN_PSETS; b++) hipFree(c->csh[b]);
+    hipFree(c->qs8);
+    for (int b = 0; b < KNN_PSETS; b++) hipFree(c->cs8[b]);
     if (c->ev_in) hipEventDestroy(c->ev_in);
     hipFree(c->qthr);
     hipFree(c->st_d);
@@ -346,6 +353,8 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
         if ((f == KNN_KP || f == KNN_KP_M || f == KNN_KP_L) && k <= f) c->kp = f;
     }
     c->kl = knn_kl_for(c->kp);
+    c->lpq = 4;
+    c->klx = c->kl;
     c->xord = getenv("KNN_XCD_ORDER") ? atoi(getenv("KNN_XCD_ORDER")) != 0 : 0;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
 
@@ -397,6 +406,7 @@ int knn_ctx_destroy(knn_ctx_t *c)
 int knn_ctx_contraction_bits(const knn_ctx_t *c)
 {
     if (!c) return 0;
+    if (c->i8) return 8;
     return c->h16 ? 16 : (c->dtype == KNN_F64 ? 64 : 32);
 }
 
@@ -429,8 +439,29 @@ static int knn_h16_exact(const double *meta, size_t n, int dtype)
            (double)n * rg * rg <= 16777216.0;
 }
 
-int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_base,
-                  const double *d_meta, void *stream)
+/* INT mode for the element type (every key of the search exact) with every
+ * value inside a window of 256 integers (hi - lo <= 255, lo = -meta[MAXNEG],
+ * hi = meta[MAXPOS]) and n <= KNN_I8_MAX_N: x - (lo + 128) is an exact int8
+ * and the int8 MFMA contraction gives d^2 exactly (knn_i8.hip). */
+static int knn_i8_exact(const double *meta, size_t n, int dtype)
+{
+    if (n > KNN_I8_MAX_N || meta[KNN_META_NONFINITE] != 0.0 || meta[KNN_META_NONINT] != 0.0) return 0;
+    if (!(meta[KNN_META_MAXNORM] < (dtype == KNN_F64 ? 1e290 : 1e37))) return 0;
+    const double mx = meta[KNN_META_MAXABS];
+    const double rg = meta[KNN_META_MAXPOS] + meta[KNN_META_MAXNEG];
+    if (!(rg <= 255.0)) return 0;
+    if (dtype == KNN_F64) return mx * mx <= 2251799813685248.0 / (4.0 * (double)n);
+    return (double)n * mx * mx <= 8388608.0 && (double)n * rg * rg <= 16777216.0;
+}
+
+static int env_on(const char *name)
+{
+    const char *e = getenv(name);
+    return e && e[0] == '1';
+}
+
+int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_base,
+                       const double *d_meta, const double *h_meta, void *stream)
 {
     if (!c || !d_qblock || !d_meta || q_cap < c->nq) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
@@ -446,22 +477,40 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
     c->merged = 0;
     c->nfail = 0;
     c->h16 = 0;
-    {
-        /* one 64-byte read of the reduced meta per search picks the
-         * contraction: fp16 MFMA when it is exact (knn_h16_exact) */
-        const char *off = getenv("KNN_NO_H16");
-        if (!(off && off[0] == '1')) {
-            double hm[KNN_META_DOUBLES];
+    c->i8 = 0;
+    /* the contraction for this search from the reduced meta: int8 MFMA on
+     * byte blocks, else fp16 MFMA, when exact for the data (KNN_NO_I8=1 /
+     * KNN_NO_H16=1 disable them).  A caller that holds the host copy of
+     * the meta (the ring drivers, after their all-reduce) passes it; else
+     * one 64-byte read. */
+    const int no_i8 = env_on("KNN_NO_I8"), no_h16 = env_on("KNN_NO_H16");
+    if (!(no_i8 && no_h16)) {
+        double hm[KNN_META_DOUBLES];
+        if (!h_meta) {
             HIPCHK(hipMemcpyAsync(hm, d_meta, sizeof(hm), hipMemcpyDeviceToHost, (hipStream_t)stream));
             HIPCHK(hipStreamSynchronize((hipStream_t)stream));
-            c->h16 = knn_h16_exact(hm, c->n, c->dtype);
+            h_meta = hm;
         }
+        c->i8 = !no_i8 && knn_i8_exact(h_meta, c->n, c->dtype);
+        c->h16 = !c->i8 && !no_h16 && knn_h16_exact(h_meta, c->n, c->dtype);
     }
+    c->lpq = c->i8 ? 2 : 4;
+    c->klx = c->i8 ? knn_i8_kl(c->kp) : c->kl;
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
      * element fragments in the kernel instead) */
-    const char *nosh = getenv("KNN_NO_SHADOW");
-    c->shadow = c->h16 && !(nosh && nosh[0] == '1');
-    if (c->shadow) {
+    c->shadow = c->i8 ? 2 : (c->h16 && !env_on("KNN_NO_SHADOW"));
+    if (c->i8) {
+        const size_t need = knn_s8_bytes(q_cap, c->n);
+        if (need > c->qs8_bytes) {
+            HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+            hipFree(c->qs8);
+            c->qs8 = NULL;
+            c->qs8_bytes = 0;
+            if (hipMalloc(&c->qs8, need) != hipSuccess) return KNN_ERR_NOMEM;
+            c->qs8_bytes = need;
+        }
+        RCHK(knn_launch_shadow8(c->qs8, d_qblock, c->dtype, c->q_rows_pad, c->n, d_meta, stream));
+    } else if (c->shadow) {
         const size_t need = c->q_rows_pad * knn_round_up(c->n, 64) * 2;
         if (need > c->qsh_bytes) {
             HIPCHK(hipStreamSynchronize((hipStream_t)stream));
@@ -478,10 +527,39 @@ int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_bas
     return KNN_OK;
 }
 
+int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_base,
+                  const double *d_meta, void *stream)
+{
+    return knn_ctx_begin_meta(c, d_qblock, q_cap, q_base, d_meta, NULL, stream);
+}
+
+size_t knn_ctx_shadow_bytes(const knn_ctx_t *c, size_t cap)
+{
+    if (!c) return 0;
+    if (c->shadow == 2) return knn_s8_bytes(cap, c->n);
+    if (c->shadow == 1) return knn_shadow_bytes(cap, c->n, c->dtype);
+    return 0;
+}
+
+int knn_ctx_shadow_pack(knn_ctx_t *c, void *d_sblock, const void *d_block, size_t cap, void *stream)
+{
+    if (!c || !d_sblock || !d_block || cap == 0) return KNN_ERR_INVALID;
+    if (c->shadow == 1) return knn_shadow_pack(d_sblock, d_block, cap, c->n, c->dtype, stream);
+    if (c->shadow != 2) return KNN_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t rp = knn_rows_pad(cap);
+    RCHK(knn_launch_shadow8(d_sblock, d_block, c->dtype, rp, c->n, c->meta, stream));
+    HIPCHK(hipMemcpyAsync((char *)d_sblock + knn_s8_norm_offset(cap, c->n) + rp * 4,
+                          (const char *)d_block + knn_block_meta_offset_dt(cap, c->n, c->dtype),
+                          KNN_META_DOUBLES * sizeof(double), hipMemcpyDeviceToDevice,
+                          (hipStream_t)stream));
+    return KNN_OK;
+}
+
 /* bytes of partial lists per corpus split (k_dist_topk -> k_merge) */
 static size_t split_bytes(const knn_ctx_t *c)
 {
-    return c->nq_pad * (4 * (size_t)c->kl * (sizeof(double) + sizeof(int)) + sizeof(double));
+    return c->nq_pad * ((size_t)c->lpq * c->klx * (sizeof(double) + sizeof(int)) + sizeof(double));
 }
 
 #define KNN_PART_BUDGET ((size_t)2 << 30) /* partial-list bytes above one split */
@@ -530,10 +608,10 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     const long ntiles = (long)((nc + KNN_TC - 1) / KNN_TC);
     if (env && atoi(env) > 0) {
         int s = atoi(env);
-        return s > KNN_MAX_SPLITS ? KNN_MAX_SPLITS : s;
+        return s > KNN_MAX_LISTS / c->lpq ? KNN_MAX_LISTS / c->lpq : s;
     }
-    if (c->split_nc == nc && c->split_best > 0) return c->split_best;
-    int smax = KNN_MAX_SPLITS;
+    if (c->split_nc == nc && c->split_lpq == c->lpq && c->split_best > 0) return c->split_best;
+    int smax = KNN_MAX_LISTS / c->lpq;
     const size_t per = split_bytes(c);
     if (per > 0 && KNN_PART_BUDGET / per < (size_t)smax)
         smax = KNN_PART_BUDGET / per > 1 ? (int)(KNN_PART_BUDGET / per) : 1;
@@ -549,6 +627,7 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         }
     }
     c->split_nc = nc;
+    c->split_lpq = c->lpq;
     c->split_best = best;
     return best;
 }
@@ -561,7 +640,20 @@ static int ensure_part_buffers(knn_ctx_t *c, int nsplit, int set, int off)
 {
     const int pr = set >> 1;
     const int need = (set & 1) ? off + nsplit : 2 * nsplit;
-    const size_t per = c->nq_pad * 4 * (size_t)c->kl;
+    const size_t per = c->nq_pad * (size_t)c->lpq * c->klx;
+    if (per != c->pp_per[pr]) {
+        /* list shape changed (another kernel): the old sets hold nothing pending */
+        if (c->pend) return KNN_ERR_INVALID;
+        if (c->pp_cap[pr]) HIPCHK(hipStreamSynchronize(c->ms));
+        hipFree(c->pp_d[pr]);
+        hipFree(c->pp_i[pr]);
+        hipFree(c->pp_T[pr]);
+        c->pp_d[pr] = NULL;
+        c->pp_i[pr] = NULL;
+        c->pp_T[pr] = NULL;
+        c->pp_cap[pr] = 0;
+        c->pp_per[pr] = per;
+    }
     if (need > c->pp_cap[pr]) {
         if ((set & 1) && c->pend) return KNN_ERR_INVALID;   /* caller merges first */
         /* the pair may still be read by an earlier step's merge */
@@ -594,7 +686,7 @@ static int launch_merge_sets(knn_ctx_t *c, int set, int nsets, int nsplit_total,
                              size_t c_base, size_t nc)
 {
     RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
-                          nsplit_total, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x,
+                          nsplit_total, c->lpq, c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x,
                           c->st_i, c->st_T, c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n,
                           c->meta, c->ms));
     c->merged = 1;
@@ -644,7 +736,8 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
      * block rows in k_merge) -- half the merges, which at P = 8 cost about
      * as much as the contraction.  KNN_NO_PAIR=1 disables it. */
     const char *np_env = getenv("KNN_NO_PAIR");
-    const int can_pair = c->h16 && nsplit <= 7 && !(np_env && np_env[0] == '1');
+    const int can_pair = (c->h16 || c->i8) && 2 * c->lpq * nsplit + 1 <= 64 &&
+                         !(np_env && np_env[0] == '1');
     int pairing = 0;
     if ((set & 1) && c->pend) {
         pairing = can_pair && nsplit == c->pend_nsplit;
@@ -667,7 +760,17 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
     if (c->nstep >= KNN_PSETS) HIPCHK(hipStreamWaitEvent(ds, c->ev_m[set], 0));
     const void *csh = d_sblock, *cn_ptr = NULL;
-    if (d_sblock) {
+    if (c->i8) {
+        if (!d_sblock && d_cblock == c->qblk && knn_rows_pad(c->block_cap) == c->q_rows_pad) {
+            csh = c->qs8;   /* the query block itself (P = 1): its byte block exists */
+        } else if (!d_sblock) {
+            if (!c->cs8[set] && hipMalloc(&c->cs8[set], knn_s8_bytes(c->block_cap, c->n)) != hipSuccess)
+                return KNN_ERR_NOMEM;
+            RCHK(knn_launch_shadow8(c->cs8[set], d_cblock, c->dtype, knn_rows_pad(c->block_cap), c->n,
+                                    c->meta, ds));
+            csh = c->cs8[set];
+        }
+    } else if (d_sblock) {
         cn_ptr = (const char *)d_sblock + knn_shadow_norm_offset(c->block_cap, c->n);
     } else if (c->shadow && d_cblock == c->qblk && knn_rows_pad(nc) <= c->q_rows_pad) {
         csh = c->qsh;   /* the query block itself (P = 1): its shadow exists */
@@ -686,13 +789,19 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
         ev = &c->prof_ev[3 * c->prof_pending++];
         HIPCHK(hipEventRecord(ev[0], ds));
     }
-    RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, cblk,
-                              knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta, nsplit,
-                              c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr,
-                              c->qsh, csh, cn_ptr,
-                              (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0) |
-                                  (c->shadow ? KNN_DIST_SHADOW : 0),
-                              ds));
+    if (c->i8)
+        RCHK(knn_launch_dist_i8(c->kp, c->k, c->qs8, c->q_rows_pad, c->q_base, (int)c->nq, csh,
+                                knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, nsplit,
+                                c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad,
+                                c->qthr, ds));
+    else
+        RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq,
+                                  cblk, knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta,
+                                  nsplit, c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad,
+                                  c->qthr, c->qsh, csh, cn_ptr,
+                                  (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0) |
+                                      (c->shadow ? KNN_DIST_SHADOW : 0),
+                                  ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
     HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));
@@ -747,7 +856,8 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     HIPCHK(hipStreamWaitEvent(s, c->ev_m[(c->nstep - 1) % KNN_PSETS], 0));   /* the last merge */
     RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
                              (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
-                             c->fail_list, c->mode_dev, c->fbound, stream));
+                             c->fail_list, c->mode_dev, c->fbound, env_on("KNN_FORCE_RESCAN"),
+                             stream));
     int host[2];
     HIPCHK(hipMemcpyAsync(&host[0], c->fail_count, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&host[1], c->mode_dev, sizeof(int), hipMemcpyDeviceToHost, s));

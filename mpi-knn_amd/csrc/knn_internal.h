@@ -65,6 +65,21 @@ static inline int knn_rescan_chunks(int nfail)
     return c > 32 ? 32 : (c < 1 ? 1 : c);
 }
 static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
+
+/* Byte block (knn_i8.hip): the int8 form of a packed block for the int8
+ * MFMA contraction of 8-bit-window integer data.  Rows of round_up(n, 32)
+ * bytes (x - o, o = 128 - meta[MAXNEG]), then one int32 |x - o|^2 per row in
+ * the per-tile order of i8_norm_pos, then the block's 8 meta doubles. */
+#define KNN_I8_MAX_N 896  /* 7 chunks of 128 features: queries stay in VGPRs */
+#define KNN_I8_KL   24    /* per-lane list length, k <= 32 (2 lanes a query) */
+#define KNN_I8_KL_L 48    /* k <= 128                                         */
+static inline size_t knn_s8_rs(size_t n) { return knn_round_up(n ? n : 1, 32); }
+static inline size_t knn_s8_norm_offset(size_t cap, size_t n) { return knn_rows_pad(cap) * knn_s8_rs(n); }
+static inline size_t knn_s8_bytes(size_t cap, size_t n)
+{
+    return knn_round_up(knn_s8_norm_offset(cap, n) + knn_rows_pad(cap) * 4 + 8 * sizeof(double), 16);
+}
+static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL : KNN_I8_KL_L; }
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
 {
     return knn_round_up(n ? n : 1, 128 / knn_esize(dtype));
@@ -87,8 +102,17 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
 /* fp16 shadow rows (round_up(n, 64) halves a row) of a packed block */
 int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
+/* knn_i8.hip: element block -> byte block (meta = the reduced meta) and the
+ * int8 distance + top-k kernel (partial lists [split][query][2][kl]) */
+int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,
+                       const double *meta, void *stream);
+int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_pad, size_t q_base, int nq,
+                       const void *csh, size_t c_rows_pad, size_t c_base, int nc, int n, int nsplit,
+                       double *part_d, int *part_i, double *part_T, int nq_pad, double *qthr,
+                       void *stream);
 int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *part_i,
-                     const double *part_T, int nsplit, int nq, int nq_pad, int first_step,
+                     const double *part_T, int nsplit, int lpq, int kl, int nq, int nq_pad,
+                     int first_step,
                      double *st_d, double *st_x, int *st_i, double *st_T, const void *qblk,
                      size_t q_rows_pad, const void *cblk, size_t c_base, int nc, int n,
                      const double *meta, void *stream);
@@ -96,7 +120,7 @@ int knn_launch_finalize(int dtype, int kp, const double *st_d, const double *st_
                         const double *st_T, const void *qblk, size_t q_rows_pad,
                         int nq, int n, int k, const double *meta,
                         knn_neighbour_t *out, int *fail_count, int *fail_list,
-                        int *mode_out, double *fbound, void *stream);
+                        int *mode_out, double *fbound, int force_fail, void *stream);
 int knn_launch_rescan_init(int kp, double *rs_d, int *rs_i, int nfail, void *stream);
 int knn_launch_rescan_step(int dtype, int kp, const int *fail_list, int nfail,
                            const double *fbound, const void *qblk, const void *cblk,

@@ -20,16 +20,7 @@
 //                certificate could not clear.
 //
 // Layout and roofline notes: DESIGN.md sec.4.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include "knn_internal.h"
-
-typedef double dbl4 __attribute__((ext_vector_type(4)));
-typedef double dbl2 __attribute__((ext_vector_type(2)));
-typedef float flt4 __attribute__((ext_vector_type(4)));
-#define LDS_AS __attribute__((address_space(3)))
-
-static constexpr double KNN_INF = __builtin_inf();
+#include "knn_device.h"
 
 // ---------------------------------------------------------------------------
 // Element-type traits.  A staged chunk is 128 bytes of every row: 16 fp64
@@ -265,39 +256,6 @@ __global__ __launch_bounds__(256) void k_norms(T *__restrict__ blk, size_t rows,
 }
 
 // ---------------------------------------------------------------------------
-// Register top-KP list: L ascending, insertion after equal keys (the lane's
-// candidates arrive in increasing row order, so this is the reference's
-// stable "lower index first" tie rule).  d >= L[KP-1] (incl. +inf,
-// NaN) is a no-op, so lanes without a candidate run it harmlessly.
-// ---------------------------------------------------------------------------
-template <int KP, typename T>
-__device__ __forceinline__ void list_insert(T (&L)[KP], int (&I)[KP], T d, int id)
-{
-    bool c_hi = d < L[KP - 1];
-#pragma unroll
-    for (int e = KP - 1; e >= 0; e--) {
-        bool c_lo = (e > 0) ? (d < L[e > 0 ? e - 1 : 0]) : false;
-        T t = c_lo ? L[e > 0 ? e - 1 : 0] : d;
-        int ti = c_lo ? I[e > 0 ? e - 1 : 0] : id;
-        L[e] = c_hi ? t : L[e];
-        I[e] = c_hi ? ti : I[e];
-        c_hi = c_lo;
-    }
-}
-
-__device__ __forceinline__ void wave_argmin(double &d, int &i)
-{
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        double od = __shfl_xor(d, off);
-        int oi = __shfl_xor(i, off);
-        bool take = (od < d) || (od == d && oi < i);
-        d = take ? od : d;
-        i = take ? oi : i;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // k_dist_topk
 //
 // Workgroup: 512 threads = 8 waves; 128 queries (wave w: queries 16w..16w+15)
@@ -350,41 +308,6 @@ __device__ __forceinline__ void wave_argmin(double &d, int &i)
 // ---------------------------------------------------------------------------
 #define KNN_NST 4
 __device__ unsigned long long knn_dbg_rounds[256];   // tuning harness only (EPI 3)
-
-// LDS-DMA issue as inline asm (guide: glds16_asm).  Written through
-// __builtin_amdgcn_global_load_lds, the loads make hipcc's waitcnt pass treat
-// every later LDS read as racing a pending FLAT access and emit lgkmcnt(0)
-// ahead of each segment's first MFMA; hidden from it, their completion is
-// counted by this kernel's own `s_waitcnt vmcnt(N)`.  M0 (the wave-uniform
-// LDS destination) is written and restored inside the statement.
-// Buffer form: wave-uniform base in a 128-bit descriptor (raw, stride 0),
-// 32-bit per-lane byte offset (half the address payload of the global form).
-typedef int knn_v4i __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ knn_v4i knn_rsrc(const void *base)
-{
-    const unsigned long long a = (unsigned long long)(uintptr_t)base;
-    knn_v4i r;
-    r.x = (int)(unsigned)a;
-    r.y = (int)((unsigned)(a >> 32) & 0xffffu);
-    r.z = -1;                 // num_records: no bounds check in practice
-    r.w = 0x00020000;
-    return r;
-}
-__device__ __forceinline__ void bglds16(knn_v4i rsrc, unsigned voff, unsigned lds_dst)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
-}
-// 4-byte global form (corpus-norm slices: per-lane permuted gather)
-__device__ __forceinline__ void glds4(const void *src, unsigned lds_dst)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
-}
 
 // EPI != 1 / ABL != 0 exist only for the tuning harness (tools/probe/kbench):
 // EPI 0 skips the top-k insertion, EPI 3 counts insertion rounds per tile
@@ -892,17 +815,18 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
 }
 
 // ---------------------------------------------------------------------------
-// k_merge: one wave per query.  Lane j < 4*nsplit owns partial list j,
-// lane 4*nsplit the running state; KP+1 rounds of a wave argmin over the
+// k_merge: one wave per query.  Lane j < lpq*nsplit owns partial list j
+// (lpq lists per query and split: 4 from k_dist_topk, 2 from k_dist_topk_i8),
+// lane lpq*nsplit the running state; KP+1 rounds of a wave argmin over the
 // heads select the new state (KP entries by (d^2, idx)) and the smallest
 // dropped value, which lowers the rejection bound T.  GEMM mode: entries
 // new in this step get their exact reference-order S from the resident
 // block (the only step at which their rows are on this device).
 // ---------------------------------------------------------------------------
-template <typename TE, int KL, int KP>
+template <typename TE, int KP>
 __global__ __launch_bounds__(256) void k_merge(
     const double *__restrict__ part_d, const int *__restrict__ part_i,
-    const double *__restrict__ part_T, int nsplit, int nq, int nq_pad, int first_step,
+    const double *__restrict__ part_T, int nsplit, int lpq, int kl, int nq, int nq_pad, int first_step,
     double *__restrict__ st_d, double *__restrict__ st_x, int *__restrict__ st_i,
     double *__restrict__ st_T, const TE *__restrict__ qblk, size_t qnorm_off,
     const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
@@ -912,17 +836,17 @@ __global__ __launch_bounds__(256) void k_merge(
     const int q = blockIdx.x * 4 + wave;
     if (q >= nq) return;
     const int mode = knn_mode<TE>(meta, n);
-    const int nl = 4 * nsplit;
+    const int nl = lpq * nsplit;   // partial lists: [split][query][lpq][kl]
 
     const double *src_d = nullptr;
     const int *src_i = nullptr;
     int len = KP;
     if (lane < nl) {
-        const int s = lane >> 2, gg = lane & 3;
-        const size_t base = (((size_t)s * nq_pad + q) * 4 + gg) * KL;
+        const int s = lane / lpq, gg = lane - s * lpq;
+        const size_t base = (((size_t)s * nq_pad + q) * lpq + gg) * kl;
         src_d = part_d + base;
         src_i = part_i + base;
-        len = KL;
+        len = kl;
     } else if (lane == nl && !first_step) {
         src_d = st_d + (size_t)q * KP;
         src_i = st_i + (size_t)q * KP;
@@ -1051,7 +975,7 @@ __global__ __launch_bounds__(256) void k_finalize(
     const TE *__restrict__ qnorm, int nq, int n, int k,
     const double *__restrict__ meta, knn_neighbour_t *__restrict__ out,
     int *__restrict__ fail_count, int *__restrict__ fail_list, int *__restrict__ mode_out,
-    double *__restrict__ fbound)
+    double *__restrict__ fbound, int force_fail)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + wave;
@@ -1060,7 +984,7 @@ __global__ __launch_bounds__(256) void k_finalize(
     if (q >= nq) return;
     knn_neighbour_t *o = out + (size_t)q * k;
 
-    if (mode == KNN_MODE_SCAN) {
+    if (mode == KNN_MODE_SCAN || force_fail) {   // force_fail: tests of the rescan pass
         if (lane == 0) {
             fail_list[atomicAdd(fail_count, 1)] = q;
             fbound[q] = KNN_INF;
@@ -1682,20 +1606,20 @@ extern "C" int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, 
 }
 
 extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *part_i,
-                                const double *part_T, int nsplit, int nq, int nq_pad,
+                                const double *part_T, int nsplit, int lpq, int kl, int nq, int nq_pad,
                                 int first_step, double *st_d, double *st_x, int *st_i,
                                 double *st_T, const void *qblk, size_t q_rows_pad,
                                 const void *cblk, size_t c_base, int nc, int n,
                                 const double *meta, void *stream)
 {
-    if (4 * nsplit + 1 > 64 || k <= 0 || k > kp) return KNN_ERR_INVALID;
+    if (lpq < 1 || kl < 1 || lpq * nsplit + 1 > 64 || k <= 0 || k > kp) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
     const size_t qn_off = q_rows_pad * (size_t)np;
     const dim3 grid((unsigned)((nq + 3) / 4));
     hipStream_t s = (hipStream_t)stream;
 #define CALL(T, KL, KP)                                                                         \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KL, KP>), grid, dim3(256), 0, s, part_d, part_i, \
-                       part_T, nsplit, nq, nq_pad, first_step, st_d, st_x, st_i, st_T,            \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP>), grid, dim3(256), 0, s, part_d, part_i,    \
+                       part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x, st_i, st_T,   \
                        (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n, np, meta, k);    \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
@@ -1706,7 +1630,7 @@ extern "C" int knn_launch_finalize(int dtype, int kp, const double *st_d, const 
                                    const int *st_i, const double *st_T, const void *qblk,
                                    size_t q_rows_pad, int nq, int n, int k, const double *meta,
                                    knn_neighbour_t *out, int *fail_count, int *fail_list,
-                                   int *mode_out, double *fbound, void *stream)
+                                   int *mode_out, double *fbound, int force_fail, void *stream)
 {
     if (k <= 0 || k > kp) return KNN_ERR_INVALID;
     const size_t off = q_rows_pad * knn_n_pad_dt(n, dtype);
@@ -1715,7 +1639,7 @@ extern "C" int knn_launch_finalize(int dtype, int kp, const double *st_d, const 
 #define CALL(T, KL, KP)                                                                        \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_finalize<T, KP>), grid, dim3(256), 0, s, st_d, st_x,   \
                        st_i, st_T, (const T *)qblk + off, nq, n, k, meta, out, fail_count,       \
-                       fail_list, mode_out, fbound);                                             \
+                       fail_list, mode_out, fbound, force_fail);                                 \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL

@@ -15,6 +15,11 @@
  * one is being contracted.  Every device visits all P blocks exactly once;
  * results are byte-identical to the 1-GPU path (merge order is by (d, idx)).
  * The meta of all blocks is combined with one ncclAllReduce(max).
+ *
+ * The hop is a transport: RCCL over the node's GPUs, or (KNN_RING_LOOPBACK=1)
+ * a loopback of P virtual ranks on device 0 whose hop is P device copies on
+ * one "fabric" stream -- the same schedule, buffers, events and lag rule,
+ * so the P >= 2 ring is testable on a one-GPU box (tests/test_gpu_ring_rotation.py).
  */
 #include "knn_internal.h"
 
@@ -26,6 +31,12 @@
 
 #define KNN_RING_MAX 64
 #define NRX (KNN_STEP_LAG + 2)  /* receive buffers per device */
+
+enum { RING_RCCL = 0, RING_LOOPBACK = 1 };
+typedef struct {
+    int kind;
+    hipStream_t fabric;         /* loopback: every hop's copies, in hop order */
+} ring_transport_t;
 
 typedef struct {
     int dev;
@@ -50,8 +61,27 @@ static double now_s(void)
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-static int ring_hop(ring_dev_t *d, int P, size_t bytes)
+/* Loopback hop: virtual rank g's cur -> rank g+1's nxt, all on device 0.
+ * The fabric stream waits for every rank's compute-side event (its nxt is
+ * free, its own block is packed) and runs the copies in hop order, so a
+ * block forwarded at hop h was received at hop h-1 on the same stream. */
+static int ring_hop_loopback(ring_dev_t *d, int P, size_t bytes, ring_transport_t *t)
 {
+    if (hipSetDevice(d[0].dev) != hipSuccess) return KNN_ERR_HIP;
+    for (int g = 0; g < P; g++)
+        if (hipStreamWaitEvent(t->fabric, d[g].ev_comp, 0) != hipSuccess) return KNN_ERR_HIP;
+    for (int g = 0; g < P; g++)
+        if (hipMemcpyAsync(d[(g + 1) % P].nxt, d[g].cur, bytes, hipMemcpyDeviceToDevice, t->fabric) !=
+            hipSuccess)
+            return KNN_ERR_HIP;
+    for (int g = 0; g < P; g++)
+        if (hipEventRecord(d[g].ev_comm, t->fabric) != hipSuccess) return KNN_ERR_HIP;
+    return KNN_OK;
+}
+
+static int ring_hop(ring_dev_t *d, int P, size_t bytes, ring_transport_t *t)
+{
+    if (t->kind == RING_LOOPBACK) return ring_hop_loopback(d, P, bytes, t);
     /* nxt[g] was read by step s-1's compute: the comm waits for it. */
     for (int g = 0; g < P; g++) {
         if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
@@ -76,11 +106,11 @@ static int ring_hop(ring_dev_t *d, int P, size_t bytes)
 /* One full rotation: at step s device g folds block (g - off - s) mod P,
  * where off says how far the blocks have already moved. */
 static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int off,
-                     int rescan)
+                     int rescan, ring_transport_t *t)
 {
     int rc;
     for (int s = 0; s < P; s++) {
-        if (s < P - 1 && (rc = ring_hop(d, P, bytes))) return rc;
+        if (s < P - 1 && (rc = ring_hop(d, P, bytes, t))) return rc;
         for (int g = 0; g < P; g++) {
             const int b = ((g - off - s) % P + P) % P;
             const size_t base = (size_t)b * R;
@@ -108,15 +138,32 @@ static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int
     return KNN_OK;
 }
 
+/* Largest P' <= P whose ceil(m/P')-row blocks are all non-empty (results do
+ * not depend on the block count; the reference CLIs accept any procs). */
+static int ring_blocks_for(size_t m, int P)
+{
+    if ((size_t)P > m) P = (int)m;
+    while (P > 1 && (size_t)(P - 1) * ((m + P - 1) / P) >= m) P--;
+    return P < 1 ? 1 : P;
+}
+
 int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k, int ngpus,
                          int dtype, knn_neighbour_t *out, double *seconds)
 {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KNN_ERR_NODEVICE;
-    if (ngpus > ndev || ngpus > KNN_RING_MAX) return KNN_ERR_NODEVICE;
-    const int P = ngpus;
+    if (ngpus < 1) return KNN_ERR_INVALID;
+    ring_transport_t tr;
+    memset(&tr, 0, sizeof(tr));
+    const char *lb = getenv("KNN_RING_LOOPBACK");
+    tr.kind = (lb && lb[0] == '1') ? RING_LOOPBACK : RING_RCCL;
+    /* RCCL: one block per GPU, at most the GPUs present (procs > GPUs runs on
+     * every GPU); loopback: P virtual ranks on device 0 */
+    int P = ngpus;
+    if (tr.kind == RING_RCCL && P > ndev) P = ndev;
+    if (P > KNN_RING_MAX) P = KNN_RING_MAX;
+    P = ring_blocks_for(m, P);
     const size_t R = (m + P - 1) / P;
-    if (R == 0 || (size_t)(P - 1) * R >= m) return KNN_ERR_INVALID; /* every block non-empty */
     const size_t bytes = knn_block_bytes_dt(R, n, dtype);
     if (bytes == 0) return KNN_ERR_INVALID;
 
@@ -124,17 +171,24 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
     memset(d, 0, sizeof(d));
     int devs[KNN_RING_MAX];
     ncclComm_t comms[KNN_RING_MAX];
+    memset(comms, 0, sizeof(comms));
     int rc = KNN_OK;
-    for (int g = 0; g < P; g++) devs[g] = g;
-    if (ncclCommInitAll(comms, P, devs) != ncclSuccess) return KNN_ERR_RCCL;
+    for (int g = 0; g < P; g++) devs[g] = tr.kind == RING_LOOPBACK ? 0 : g;
+    if (tr.kind == RING_RCCL) {
+        if (ncclCommInitAll(comms, P, devs) != ncclSuccess) return KNN_ERR_RCCL;
+    } else {
+        if (hipSetDevice(0) != hipSuccess ||
+            hipStreamCreateWithFlags(&tr.fabric, hipStreamNonBlocking) != hipSuccess)
+            return KNN_ERR_HIP;
+    }
 
     for (int g = 0; g < P && !rc; g++) {
         ring_dev_t *e = &d[g];
-        e->dev = g;
+        e->dev = devs[g];
         e->comm = comms[g];
         e->base = (size_t)g * R;
         e->rows = (e->base + R <= m) ? R : m - e->base;
-        if (hipSetDevice(g) != hipSuccess) { rc = KNN_ERR_HIP; break; }
+        if (hipSetDevice(e->dev) != hipSuccess) { rc = KNN_ERR_HIP; break; }
         if (hipStreamCreateWithFlags(&e->cs, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&e->ms, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&e->ev_comp, hipEventDisableTiming) != hipSuccess ||
@@ -160,16 +214,16 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             he = hipMemcpy(e->src, X + e->base * n, e->rows * n * sizeof(double),
                            hipMemcpyHostToDevice);
         if (he != hipSuccess) { rc = KNN_ERR_HIP; break; }
-        rc = knn_ctx_create_dt(&e->ctx, g, e->rows, n, R, k, dtype);
+        rc = knn_ctx_create_dt(&e->ctx, e->dev, e->rows, n, R, k, dtype);
     }
     for (int g = 0; g < P && !rc; g++)
-        if (hipSetDevice(g) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = KNN_ERR_HIP;
+        if (hipSetDevice(d[g].dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = KNN_ERR_HIP;
 
     const double t0 = now_s();
     /* pack own block (blk:100-109) and reduce the meta over the ring */
     for (int g = 0; g < P && !rc; g++) {
         ring_dev_t *e = &d[g];
-        hipSetDevice(g);
+        hipSetDevice(e->dev);
         e->cur = e->qb;
         e->hop = 0;
         e->nxt = e->rx[0];
@@ -180,52 +234,81 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
                                   e->cs) != hipSuccess)
             rc = KNN_ERR_HIP;
     }
-    if (!rc) {
+    /* the reduced meta, also on the host: it picks the contraction for every
+     * rank (knn_ctx_begin_meta, no per-rank read-back) */
+    double hm[KNN_META_DOUBLES];
+    if (!rc && tr.kind == RING_RCCL) {
         if (ncclGroupStart() != ncclSuccess) rc = KNN_ERR_RCCL;
         for (int g = 0; g < P && !rc; g++)
             if (ncclAllReduce(d[g].meta, d[g].meta, KNN_META_DOUBLES, ncclFloat64, ncclMax,
                               d[g].comm, d[g].cs) != ncclSuccess)
                 rc = KNN_ERR_RCCL;
         if (ncclGroupEnd() != ncclSuccess && !rc) rc = KNN_ERR_RCCL;
+        if (!rc && (hipSetDevice(d[0].dev) != hipSuccess ||
+                    hipMemcpyAsync(hm, d[0].meta, sizeof(hm), hipMemcpyDeviceToHost, d[0].cs) != hipSuccess ||
+                    hipStreamSynchronize(d[0].cs) != hipSuccess))
+            rc = KNN_ERR_HIP;
+    } else if (!rc) {
+        /* loopback: max-reduce on the host (meta words are >= 0 or +inf) */
+        for (int x = 0; x < KNN_META_DOUBLES; x++) hm[x] = 0.0;
+        for (int g = 0; g < P && !rc; g++) {
+            double gm[KNN_META_DOUBLES];
+            if (hipMemcpyAsync(gm, d[g].meta, sizeof(gm), hipMemcpyDeviceToHost, d[g].cs) != hipSuccess ||
+                hipStreamSynchronize(d[g].cs) != hipSuccess) {
+                rc = KNN_ERR_HIP;
+                break;
+            }
+            for (int x = 0; x < KNN_META_DOUBLES; x++) hm[x] = gm[x] > hm[x] ? gm[x] : hm[x];
+        }
+        for (int g = 0; g < P && !rc; g++)
+            if (hipMemcpyAsync(d[g].meta, hm, sizeof(hm), hipMemcpyHostToDevice, d[g].cs) != hipSuccess)
+                rc = KNN_ERR_HIP;
     }
     for (int g = 0; g < P && !rc; g++) {
-        hipSetDevice(g);
-        rc = knn_ctx_begin(d[g].ctx, d[g].qb, R, d[g].base, d[g].meta, d[g].cs);
+        hipSetDevice(d[g].dev);
+        rc = knn_ctx_begin_meta(d[g].ctx, d[g].qb, R, d[g].base, d[g].meta, hm, d[g].cs);
         if (!rc && hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
     }
-    if (!rc) rc = ring_pass(d, P, R, m, bytes, 0, 0);
+    if (!rc) rc = ring_pass(d, P, R, m, bytes, 0, 0, &tr);
     size_t unresolved_total = 0;
     for (int g = 0; g < P && !rc; g++) {
         size_t u = 0;
-        hipSetDevice(g);
+        hipSetDevice(d[g].dev);
         rc = knn_ctx_end(d[g].ctx, d[g].d_out, &u, d[g].cs);
         unresolved_total += u;
     }
     if (!rc && unresolved_total) {
         /* A pass makes P-1 hops, so device g now holds block g+1; rotate
-         * once more for the exact rescan of uncertified queries. */
+         * once more for the exact rescan of uncertified queries
+         * (KNN_FORCE_RESCAN=1: every query, for tests). */
         for (int g = 0; g < P && !rc; g++) {
-            hipSetDevice(g);
+            hipSetDevice(d[g].dev);
             if (hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
         }
-        if (!rc) rc = ring_pass(d, P, R, m, bytes, P - 1, 1);
+        if (!rc) rc = ring_pass(d, P, R, m, bytes, P - 1, 1, &tr);
         for (int g = 0; g < P && !rc; g++) {
-            hipSetDevice(g);
+            hipSetDevice(d[g].dev);
             rc = knn_ctx_rescan_end(d[g].ctx, d[g].d_out, d[g].cs);
         }
     }
     for (int g = 0; g < P && !rc; g++)
-        if (hipSetDevice(g) != hipSuccess || hipStreamSynchronize(d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
+        if (hipSetDevice(d[g].dev) != hipSuccess || hipStreamSynchronize(d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
     if (seconds) *seconds = now_s() - t0;
     for (int g = 0; g < P && !rc; g++) {
-        hipSetDevice(g);
+        hipSetDevice(d[g].dev);
         if (hipMemcpy(out + d[g].base * (size_t)k, d[g].d_out,
                       d[g].rows * (size_t)k * sizeof(knn_neighbour_t), hipMemcpyDeviceToHost) != hipSuccess)
             rc = KNN_ERR_HIP;
     }
 
     for (int g = 0; g < P; g++) {
-        hipSetDevice(g);
+        hipSetDevice(d[g].dev);
+        if (d[g].cs) hipStreamSynchronize(d[g].cs);
+        if (d[g].ms) hipStreamSynchronize(d[g].ms);
+    }
+    if (tr.fabric) hipStreamSynchronize(tr.fabric);
+    for (int g = 0; g < P; g++) {
+        hipSetDevice(d[g].dev);
         if (d[g].ctx) knn_ctx_destroy(d[g].ctx);
         hipFree(d[g].qb);
         for (int b = 0; b < NRX; b++) hipFree(d[g].rx[b]);
@@ -236,7 +319,8 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         if (d[g].ev_comm) hipEventDestroy(d[g].ev_comm);
         if (d[g].cs) hipStreamDestroy(d[g].cs);
         if (d[g].ms) hipStreamDestroy(d[g].ms);
-        ncclCommDestroy(comms[g]);
+        if (tr.kind == RING_RCCL && comms[g]) ncclCommDestroy(comms[g]);
     }
+    if (tr.fabric) hipStreamDestroy(tr.fabric);
     return rc;
 }

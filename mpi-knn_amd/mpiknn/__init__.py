@@ -44,7 +44,8 @@ API_SYMBOLS = (
     "knn_ctx_create_dt", "knn_classify_device", "knn_search_mpi_compat",
     "knn_ctx_contraction_bits", "knn_wire_bytes", "knn_wire_ok", "knn_wire_pack",
     "knn_wire_unpack", "knn_shadow_bytes", "knn_shadow_norm_offset", "knn_shadow_pack",
-    "knn_ctx_shadow", "knn_ctx_step_shadow",
+    "knn_ctx_shadow", "knn_ctx_step_shadow", "knn_ctx_begin_meta", "knn_ctx_shadow_bytes",
+    "knn_ctx_shadow_pack",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -96,6 +97,9 @@ def _load():
         "knn_ctx_destroy": ([p], i),
         "knn_classify_device": ([p, sz, i, i, i, p, sz, sz, p, p, p], i),
         "knn_ctx_begin": ([p, p, sz, sz, p, p], i),
+        "knn_ctx_begin_meta": ([p, p, sz, sz, p, p, p], i),
+        "knn_ctx_shadow_bytes": ([p, sz], sz),
+        "knn_ctx_shadow_pack": ([p, p, p, sz, p], i),
         "knn_ctx_step": ([p, p, sz, sz, p], i),
         "knn_ctx_end": ([p, p, psz, p], i),
         "knn_ctx_rescan_step": ([p, p, sz, sz, p], i),
@@ -302,9 +306,16 @@ class Context:
         if not sys.is_finalizing():
             self.close()
 
-    def begin(self, d_qblock, q_cap, q_base, d_meta, stream=0):
-        _check(lib.knn_ctx_begin(self._h, d_qblock, q_cap, q_base, d_meta, stream or None),
-               "knn_ctx_begin")
+    def begin(self, d_qblock, q_cap, q_base, d_meta, stream=0, h_meta=None):
+        """knn_ctx_begin; with h_meta (host float64 copy of the reduced meta)
+        knn_ctx_begin_meta, which needs no device read-back."""
+        if h_meta is None:
+            _check(lib.knn_ctx_begin(self._h, d_qblock, q_cap, q_base, d_meta, stream or None),
+                   "knn_ctx_begin")
+        else:
+            hm = np.ascontiguousarray(h_meta, dtype=np.float64)
+            _check(lib.knn_ctx_begin_meta(self._h, d_qblock, q_cap, q_base, d_meta, _ptr(hm),
+                                          stream or None), "knn_ctx_begin_meta")
 
     def step(self, d_cblock, nc, c_base, stream=0):
         _check(lib.knn_ctx_step(self._h, d_cblock, nc, c_base, stream or None), "knn_ctx_step")
@@ -314,8 +325,16 @@ class Context:
                "knn_ctx_step_shadow")
 
     def shadow(self):
-        """1 while this search stages fp16 shadow rows (after begin)."""
+        """Shadow form of this search (after begin): 0 none, 1 fp16 shadow
+        rows, 2 byte blocks of the int8 contraction."""
         return lib.knn_ctx_shadow(self._h)
+
+    def shadow_bytes(self, cap):
+        return lib.knn_ctx_shadow_bytes(self._h, cap)
+
+    def shadow_pack(self, d_sblock, d_block, cap, stream=0):
+        _check(lib.knn_ctx_shadow_pack(self._h, d_sblock, d_block, cap, stream or None),
+               "knn_ctx_shadow_pack")
 
     def end(self, d_out, stream=0):
         u = ctypes.c_size_t()
@@ -346,5 +365,5 @@ class Context:
         return mode.value, splits.value
 
     def contraction_bits(self):
-        """64 / 32, or 16 when this fp32 search contracts on fp16 MFMA."""
+        """64 / 32, 16 (exact fp16 MFMA) or 8 (exact int8 MFMA) for this search."""
         return lib.knn_ctx_contraction_bits(self._h)

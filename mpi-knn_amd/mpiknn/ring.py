@@ -104,16 +104,20 @@ class GpuEngine:
         self.mk.wire_unpack(buf.data_ptr(), wire.data_ptr(), self.R, self.n, self.dtype,
                             self.stream())
 
-    def begin(self, q_base):
-        self.ctx.begin(self.qb.data_ptr(), self.R, q_base, self.meta.data_ptr(), self.stream())
+    def begin(self, q_base, h_meta=None):
+        self.ctx.begin(self.qb.data_ptr(), self.R, q_base, self.meta.data_ptr(), self.stream(),
+                       h_meta=h_meta)
+
+    def shadow_bytes(self):
+        return self.ctx.shadow_bytes(self.R)
 
     def shadow_block(self):
-        """own shadow block (knn_shadow_pack of the packed own block)"""
-        sb = self.mk.shadow_bytes(self.R, self.n, self.dtype)
+        """own shadow block in the search's form (knn_ctx_shadow_pack of the
+        packed own block: fp16 rows or the int8 byte block)"""
+        sb = self.ctx.shadow_bytes(self.R)
         if getattr(self, "_sqb", None) is None or self._sqb.numel() != sb:
             self._sqb = self.torch.empty(sb, dtype=self.torch.uint8, device=self.dev)
-        self.mk.shadow_pack(self._sqb.data_ptr(), self.qb.data_ptr(), self.R, self.n, self.dtype,
-                            self.stream())
+        self.ctx.shadow_pack(self._sqb.data_ptr(), self.qb.data_ptr(), self.R, self.stream())
         return self._sqb
 
     def step_shadow(self, sbuf, rows, base):
@@ -144,19 +148,21 @@ def ring_search(dist, torch, engine, rank, P, m, q_base):
     import os
     R, blocks = partition(m, P)
     wire = False
+    h_meta = None
     if P > 1:
         dist.all_reduce(engine.meta, op=dist.ReduceOp.MAX)
+        h_meta = engine.meta.cpu().numpy()   # the ring needs it on the host anyway
         wire = (os.environ.get("KNN_NO_WIRE", "0") != "1" and hasattr(engine, "wires") and
-                engine.mk.wire_ok(engine.meta.cpu().numpy()))
-    engine.begin(q_base)
-    shadow = (P > 1 and hasattr(engine, "step_shadow") and engine.ctx.shadow() == 1 and
+                engine.mk.wire_ok(h_meta))
+    engine.begin(q_base, h_meta=h_meta)
+    shadow = (P > 1 and hasattr(engine, "step_shadow") and engine.ctx.shadow() != 0 and
               os.environ.get("KNN_NO_SHADOW_RING", "0") != "1")
 
     rx = engine.rx
     # cur: the block folded next; send: what goes on the link
     state = {"cur": engine.qb, "send": engine.qb, "hop": 0}
     if shadow:
-        sb = engine.mk.shadow_bytes(engine.R, engine.n, engine.dtype)
+        sb = engine.shadow_bytes()
         own_s = engine.shadow_block()
         srx = tuple(b[:sb] for b in rx)      # shadow blocks fit the element buffers
         state["cur"] = state["send"] = own_s

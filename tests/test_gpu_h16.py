@@ -4,6 +4,7 @@ the fp32 exact-integer range, fp64 searches when every value is an integer
 with max|x| <= 256 (fp32 partial sums over 256 features stay exact, then
 fp64 accumulation).  Either way the result must be bit-identical to the
 oracle.
+Run with KNN_NO_I8=1 (the int8 path has its own tests, test_gpu_i8.py).
 Checked through bench's per-rank engine (mpiknn.ring.GpuEngine) so the
 contraction actually used is visible."""
 import numpy as np
@@ -12,6 +13,13 @@ import pytest
 import datasets
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _fp16_path(monkeypatch):
+    # 8-bit-window data now takes the int8 contraction (test_gpu_i8.py);
+    # these cases pin the fp16 one
+    monkeypatch.setenv("KNN_NO_I8", "1")
 
 
 def run_engine(X, k, dtype="f32"):

@@ -125,14 +125,13 @@ def test_nonfinite_scan_mode(knn, oracle):
 
 
 def test_ring_blocks_match_single_device(knn, oracle):
-    """The ring's per-rank work simulated on one GPU: every block count
-    gives byte-identical results to the 1-block search."""
+    """The ring's per-rank work simulated on one GPU: for every block count
+    each rank's lists equal the oracle's serial scan of its rows."""
     import torch
     import mpiknn.ring as ring
 
     for X in (datasets.mnist_like(2500, 784, seed=9)[0], datasets.digits_real()[0]):
         m, n = X.shape
-        full, _ = knn.search(X, 30)
         dev = torch.device("cuda", 0)
         Xd = torch.from_numpy(X).to(dev)
         for P in (2, 3, 8):
@@ -158,7 +157,40 @@ def test_ring_blocks_match_single_device(knn, oracle):
                         e.step(engines[b].qb, blocks[b][1], blocks[b][0], rescan=True)
                     e.rescan_end()
                 got = e.result()
-                assert_same(got, full[base:base + rows], "ring P=%d rank %d" % (P, g))
+                assert_same(got, oracle.knn(X, 30, rows=(base, rows)), "ring P=%d rank %d" % (P, g))
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+@pytest.mark.parametrize("force_rescan", [False, True])
+def test_ring_driver_loopback(knn, oracle, monkeypatch, P, force_rescan):
+    """knn_ring.c's P >= 2 schedule (ring_pass / ring_hop, the receive-buffer
+    rotation, the off = P-1 rescan rotation) with its loopback transport: P
+    virtual ranks on device 0, each hop P device copies on one fabric
+    stream.  KNN_FORCE_RESCAN=1 sends every query through the exact rescan
+    pass, so that rotation is checked too.  Against the oracle."""
+    monkeypatch.setenv("KNN_RING_LOOPBACK", "1")
+    if force_rescan:
+        monkeypatch.setenv("KNN_FORCE_RESCAN", "1")
+    for X in (datasets.mnist_like(1500, 784, seed=4)[0], datasets.digits_real()[0]):
+        ref = oracle.knn(X, 30)
+        got, _ = knn.search(X, 30, ngpus=P, layout="col")
+        assert_same(got, ref, "loopback ring P=%d" % P)
+    X = datasets.sift_like(3000, 128)
+    ref = oracle.knn(X.astype(np.float32).astype(np.float64), 32)
+    got, _ = knn.search(X, 32, ngpus=P, dtype="f32")
+    assert_same(got, ref, "loopback ring f32 P=%d" % P)
+
+
+def test_ring_driver_more_procs_than_gpus(knn, oracle):
+    """The reference's `mpi-knn-parallel_blocking 4 4` on a box with fewer
+    GPUs: knn_search runs on the GPUs present (results do not depend on the
+    block count); m=9 with P=4 (an empty ceil-block) runs too."""
+    X = datasets.mnist_like(1000, 784, seed=2)[0]
+    got, _ = knn.search(X, 30, ngpus=64)
+    assert_same(got, oracle.knn(X, 30), "ngpus=64")
+    X9 = datasets.mnist_like(9, 20, seed=3)[0]
+    got, _ = knn.search(X9, 5, ngpus=4)
+    assert_same(got, oracle.knn(X9, 5), "m=9 P=4")
 
 
 def test_rccl_ring_driver_one_gpu(knn, oracle, monkeypatch):

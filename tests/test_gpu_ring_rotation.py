@@ -6,7 +6,11 @@ send, enqueued on the caller's stream at posting time (where RCCL's stream
 would be ordered).  So the real rotation over the STEP_LAG + 2 receive buffers
 and the overlapped knn_ctx_step schedule (include/knn.h: the caller's
 stream lags KNN_STEP_LAG steps) are exercised with buffer reuse, and every rank's
-result must equal the 1-GPU search byte for byte.
+result must equal the oracle's serial scan of its rows (oracle.knn(X, k,
+rows=(base, rows)), serial:72-93) byte for byte -- in each hop form: element
+blocks, int16 wire blocks and the search's shadow form (int8 byte blocks on
+8-bit data, fp16 shadow rows on wider integers).  This replaces blk:187-244 /
+nb:196-259 with every block visited once.
 """
 import types
 
@@ -23,12 +27,22 @@ class _Req:
         pass
 
 
-def loopback_dist(torch, rank, P, packed, metas, wires, shadows):
+def loopback_dist(torch, rank, P, packed, metas, wires, engine):
     """A torch.distributed stand-in for rank `rank` of a P-ring whose packed
     blocks are `packed` (block b = rank b's own block), with wire forms
-    (mpiknn.wire_pack) `wires` and shadow blocks (mpiknn.shadow_pack)
-    `shadows`; an irecv gets the form whose size it asks for."""
+    (mpiknn.wire_pack) `wires`; shadow forms are made on first use with the
+    receiving rank's context (knn_ctx_shadow_pack: the form its search
+    folds).  An irecv gets the form whose size it asks for."""
     hop = {"n": 0}
+    shadows = {}
+
+    def shadow(b):
+        if b not in shadows:
+            sb = torch.empty(engine.ctx.shadow_bytes(engine.R), dtype=torch.uint8,
+                             device=packed[b].device)
+            engine.ctx.shadow_pack(sb.data_ptr(), packed[b].data_ptr(), engine.R, engine.stream())
+            shadows[b] = sb
+        return shadows[b]
     ns = types.SimpleNamespace()
     ns.ReduceOp = types.SimpleNamespace(MAX="max", SUM="sum")
 
@@ -50,7 +64,10 @@ def loopback_dist(torch, rank, P, packed, metas, wires, shadows):
             if fn is irecv:
                 # hop h brings the block that started on rank - h - 1
                 b = (rank - hop["n"] - 1) % P
-                forms = {t[b].numel(): t[b] for t in (packed, wires, shadows)}
+                forms = {t[b].numel(): t[b] for t in (packed, wires)}
+                if engine.ctx.shadow():
+                    sb = shadow(b)
+                    forms[sb.numel()] = sb
                 src = forms[buf.numel()]
                 buf.copy_(src, non_blocking=True)
         hop["n"] += 1
@@ -61,9 +78,10 @@ def loopback_dist(torch, rank, P, packed, metas, wires, shadows):
     return ns
 
 
-@pytest.mark.parametrize("P", [2, 4, 7])
-@pytest.mark.parametrize("kind", ["int", "real", "int-nowire", "int-noshadow"])
-def test_ring_search_rotation(knn, P, kind, monkeypatch):
+@pytest.mark.parametrize("P", [2, 4, 7, 8])
+@pytest.mark.parametrize("kind", ["int", "real", "int-nowire", "int-noshadow", "int-fp16",
+                                  "wide-int"])
+def test_ring_search_rotation(knn, oracle, P, kind, monkeypatch):
     import torch
     import mpiknn.ring as ring
 
@@ -72,9 +90,16 @@ def test_ring_search_rotation(knn, P, kind, monkeypatch):
         monkeypatch.setenv("KNN_NO_SHADOW_RING", "1")
     if kind == "int-noshadow":
         monkeypatch.setenv("KNN_NO_SHADOW_RING", "1")
-    X = datasets.mnist_like(3000, 784, seed=5)[0] if kind != "real" else datasets.digits_real()[0]
+    if kind == "int-fp16":
+        monkeypatch.setenv("KNN_NO_I8", "1")      # fp16 shadow rows on the link
+    if kind == "real":
+        X = datasets.digits_real()[0]
+    elif kind == "wide-int":                      # range 512: fp16 shadows, not int8
+        X = np.random.default_rng(P).integers(-256, 257, (2200, 300)).astype(np.float64)
+        X[40] = X[3]
+    else:
+        X = datasets.mnist_like(3000, 784, seed=5)[0]
     m, n = X.shape
-    full, _ = knn.search(X, 30)
     dev = torch.device("cuda", 0)
     Xd = torch.from_numpy(X).to(dev)
     R, blocks = ring.partition(m, P)
@@ -91,19 +116,15 @@ def test_ring_search_rotation(knn, P, kind, monkeypatch):
         w = torch.empty(knn.wire_bytes(R, n), dtype=torch.uint8, device=dev)
         knn.wire_pack(w.data_ptr(), e.qb.data_ptr(), R, n, "f64", e.stream())
         wires.append(w)
-    shadows = []
-    for e in engines:
-        sb = torch.empty(knn.shadow_bytes(R, n), dtype=torch.uint8, device=dev)
-        knn.shadow_pack(sb.data_ptr(), e.qb.data_ptr(), R, n, "f64", e.stream())
-        shadows.append(sb)
     for g, e in enumerate(engines):
         base, rows = blocks[g]
-        d = loopback_dist(torch, g, P, packed, metas, wires, shadows)
+        d = loopback_dist(torch, g, P, packed, metas, wires, e)
         ring.ring_search(d, torch, e, g, P, m, base)
         got = e.result()
-        assert np.array_equal(got["idx"], full[base:base + rows]["idx"]), (P, g)
+        ref = oracle.knn(X, 30, rows=(base, rows))
+        assert np.array_equal(got["idx"], ref["idx"]), (P, g)
         assert np.array_equal(got["distance"].view(np.uint64),
-                              full[base:base + rows]["distance"].view(np.uint64)), (P, g)
+                              ref["distance"].view(np.uint64)), (P, g)
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])

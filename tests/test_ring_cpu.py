@@ -36,7 +36,7 @@ class CpuEngine:
         self.qb[0, self.n] = rows
         self.meta[0] = float(src.abs().max())
 
-    def begin(self, q_base):
+    def begin(self, q_base, h_meta=None):
         self.q_base = q_base
         self.lists = self.O.lists_init(self.nq, self.k)
 
