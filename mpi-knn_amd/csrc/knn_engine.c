@@ -494,7 +494,7 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
         c->i8 = !no_i8 && knn_i8_exact(h_meta, c->n, c->dtype);
         c->h16 = !c->i8 && !no_h16 && knn_h16_exact(h_meta, c->n, c->dtype);
     }
-    c->lpq = c->i8 ? 2 : 4;
+    c->lpq = c->i8 ? knn_i8_lpq(c->kp) : 4;
     c->klx = c->i8 ? knn_i8_kl(c->kp) : c->kl;
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
      * element fragments in the kernel instead) */

@@ -20,7 +20,6 @@
 
 typedef int knn_v16i __attribute__((ext_vector_type(16)));
 
-#define I8_NST 4                 // corpus stages in the LDS ring
 #define I8_INF 0x7fffffff        // empty list slot / no bound
 
 // Row r of a byte block -> its slot in the norm array.  Tile t = r >> 7 owns
@@ -33,6 +32,66 @@ __device__ __forceinline__ int i8_norm_pos(int r)
     const int rr = r & 127, b = rr >> 5, w = rr & 31;
     const int j = w >> 3, h = (w >> 2) & 1, i = w & 3;
     return (r & ~127) + (((b * 2 + h) * 4 + j) * 4 + i);
+}
+
+// Insert (d, id) into the ascending register list L (after equal keys: the
+// lane's candidates arrive in row order, so ties keep the lower index,
+// SURVEY F1); d >= L[KL-1] is a no-op.  Keys: L'[e] = med3(L[e-1], L[e], d)
+// (one v_med3_i32, since L[e-1] <= L[e]); ids move where d < L[e-1].
+__device__ __forceinline__ int i8_med3(int a, int b, int c)
+{
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+template <int KL>
+__device__ __forceinline__ void i8_insert(int (&L)[KL], int (&I)[KL], int d, int id)
+{
+    // masks as (d - L) >> 31 (keys are >= 0, no overflow) and ids through
+    // v_bfi: no v_cmp -> v_cndmask lane-mask hazard (2 wait states each)
+    int m_hi = (d - L[KL - 1]) >> 31;   // -1 iff d < L[KL-1]
+#pragma unroll
+    for (int e = KL - 1; e > 0; e--) {
+        const int m_lo = (d - L[e - 1]) >> 31;
+        L[e] = i8_med3(L[e - 1], L[e], d);
+        const int in = (m_hi & id) | (~m_hi & I[e]);
+        I[e] = (m_lo & I[e - 1]) | (~m_lo & in);
+        m_hi = m_lo;
+    }
+    L[0] = d < L[0] ? d : L[0];
+    I[0] = (m_hi & id) | (~m_hi & I[0]);
+}
+
+// four LDS-DMA pieces (1 KiB each, consecutive LDS) under one M0 setup
+__device__ __forceinline__ void bglds16x4(knn_v4i rsrc, unsigned v0, unsigned v1, unsigned v2, unsigned v3,
+                                          unsigned lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %1, 0 offen lds\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %3, %1, 0 offen lds\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %4, %1, 0 offen lds\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %5, %1, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "s"(rsrc), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+                 : "memory", "scc");
+}
+
+__device__ __forceinline__ void bglds16x2(knn_v4i rsrc, unsigned v0, unsigned v1, unsigned lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %1, 0 offen lds\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %3, %1, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "s"(rsrc), "v"(v0), "v"(v1), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+                 : "memory", "scc");
 }
 
 // a where the lane's bit of m is clear, b where it is set
@@ -81,51 +140,69 @@ __global__ __launch_bounds__(256) void k_shadow8(signed char *__restrict__ dst, 
 // ---------------------------------------------------------------------------
 // k_dist_topk_i8
 //
-// Workgroup: 256 threads = 4 waves, one per SIMD; 128 queries (wave w:
-// queries 32w..32w+31) x a corpus split streamed in tiles of 128 rows and
-// chunks of 128 bytes (128 features, 4 K-steps of 32).
+// Workgroup: W waves (4 or 8), 128 queries x a corpus split streamed in
+// tiles of 128 rows and chunks of 128 bytes (128 features, 4 K-steps of 32).
+// Wave w: queries 32 (w & 3) .. +31, m-blocks (32-row blocks of the tile)
+// MB (w >> 2) .. +MB-1, MB = 16 / W.  With W = 8 two waves share each SIMD,
+// so one wave's epilogue runs beside its partner's MFMAs.
 //
-// Operands (v_mfma_i32_32x32x32_i8, D = A.B): A = 32 corpus rows (m-block
-// b of the tile), B = the wave's 32 queries; lane l (r = l & 31, h = l >> 5)
+// Operands (v_mfma_i32_32x32x32_i8, D = A.B): A = 32 corpus rows (one
+// m-block), B = the wave's 32 queries; lane l (r = l & 31, h = l >> 5)
 // supplies 16 bytes [32 s + 16 h, +16) of K-step s of row r / query r -- the
 // same byte slots on both sides, so the sum runs over every feature once.
-// D: lane l holds query r, rows 32b + 8(reg >> 2) + 4h + (reg & 3).  Each
-// query's 128 candidates of a tile sit in 2 lanes (h = 0, 1), 64 each; the
-// two lanes keep separate lists over disjoint rows and share a bound.
+// D: lane l holds query r, rows 32b + 8(reg >> 2) + 4h + (reg & 3).  A
+// query's candidates of a tile sit in 2 lanes of each wave covering it; each
+// lane keeps its own list (lpq = 2 W / 4 lists per query), bounds are shared.
 //
-// Queries are resident in registers for the whole split (4 VGPRs per K-step,
-// loaded once); the corpus streams through an I8_NST-stage LDS ring of 16 KiB
-// images filled by LDS-DMA (buffer_load_dwordx4 ... lds): wave w stages rows
-// 32w..32w+31 as 4 pieces of 8 rows x 128 B.  Image of a tile chunk: [row
-// 128][128 B], 16-byte segment s of row r at slot s ^ ((r >> 1) & 7) -- the
-// ds_read_b128 lane groups ({0-3,12-15,20-27}, ...) then hit 16 distinct
-// bank quads.  One barrier per chunk: before it each wave waits for its own
-// pieces of the chunk (counted vmcnt: the pieces of the next I8_NST - 2
-// chunks stay in flight), after it the stage freed by the previous chunk is
-// refilled.  Chunks past the split's end re-stage its last chunk, so every
-// chunk issues the same corpus pieces and the count is static.  The tile's
-// norms (512 B, permuted, i8_norm_pos) ride with its first chunk into a
-// norm ring indexed by tile % I8_NST (norm pieces only make the count more
-// conservative).
+// Queries are resident in registers (4 VGPRs per K-step, loaded once); the
+// corpus streams through an NST-stage LDS ring of 16 KiB chunk images filled
+// by LDS-DMA (buffer_load_dwordx4 ... lds), 16 pieces of 8 rows x 128 B per
+// chunk, 16 / W per wave.  Image: [row 128][128 B], 16-byte segment s of row
+// r at slot s ^ ((r >> 1) & 7): the ds_read_b128 lane groups ({0-3,12-15,
+// 20-27}, ...) hit 16 distinct bank quads.  The K-step count NKS is a
+// template bucket (>= the data's; the extra K-steps multiply zero query
+// fragments), so the chunk loop is static.  Barrier B(y) (chunk y visible) sits before the last K-step
+// of chunk y-1, after the wave's counted vmcnt for its own pieces of chunk y;
+// chunk y's first fragments then load under the last MFMAs of chunk y-1, and
+// the stage of chunk y-2 takes chunk y + NST - 2.  Chunks past the split's
+// end re-stage its last chunk (static count).  A tile's norms (512 B,
+// permuted, i8_norm_pos) ride with its first chunk into a norm ring.
 //
-// Epilogue per tile: key = |c'|^2 - 2 q'.c' (int32), one masked-free test of
-// the lane minimum against min(own KL-th, shared bound) - |q'|^2, then the
-// survivors per m-block (lowest row first: the stable tie order) through a
-// 4-level select tree into the KL-entry insertion network.  d^2 = key + |q'|^2
-// is exact, so "S != 0" (serial:86) is d^2 > 0.
+// Epilogue per tile: key = |c'|^2 - 2 q'.c' (int32) and the lane minimum
+// against min(own KL-th, shared bound) - |q'|^2; survivors, lowest row first
+// (the stable tie order), go through a select tree into a per-lane LDS
+// buffer of NB entries (d^2 = key + |q'|^2).  When some lane's buffer is
+// full the wave merges all buffers into the KL-entry register lists (one
+// entry a round through the insertion network) and refreshes the bounds, so
+// the network runs on dense rounds instead of once per survivor of the
+// busiest lane per tile.  d^2 is exact, so "S != 0" (serial:86) is d^2 > 0,
+// applied at the merge.
+//
+// ABL: ablations for the tuning harness tools/probe/kbench8 only (libknn
+// instantiates ABL = 0): 1 no epilogue, 2 keys + lane minimum only, 4 no
+// staging DMA, 8 no chunk wait/barrier, 16 no MFMA, 32 count wave-tiles with
+// survivors and insertion rounds into i8_dbg.
 // ---------------------------------------------------------------------------
-template <int KL, int NC, int WPS>
-__global__ __launch_bounds__(256, WPS) void k_dist_topk_i8(
+__device__ unsigned long long i8_dbg[4];   // tuning harness only (ABL 32)
+template <int KL, int NKS, int W, int WPS, int NST, int NB, int ABL = 0>
+__global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     const signed char *__restrict__ qsh, size_t q_rows_pad, size_t q_base, int nq,
     const signed char *__restrict__ csh, size_t c_rows_pad, size_t c_base, int nc, int rs,
     int nks, int ntiles, int nsplit, int nqb, double *__restrict__ part_d,
     int *__restrict__ part_i, double *__restrict__ part_T, int nq_pad,
     unsigned long long *__restrict__ qthr, int uj)
 {
-    constexpr int NST = I8_NST;
-    __shared__ __attribute__((aligned(16))) char smem[NST * 16384 + NST * 512];
+    constexpr int MB = 16 / W;              // m-blocks per wave
+    constexpr int PW = 16 / W;              // DMA pieces per wave per chunk
+    constexpr int LPQ = 2 * (W / 4);        // lists per query
+    constexpr int NORM0 = NST * 16384;
+    constexpr int BUF0 = NORM0 + NST * 512; // [W][NB][64] survivor d^2, then ids
+    constexpr int XB0 = BUF0 + 2 * W * NB * 256;   // W = 8: [8][32] bound exchange
+    constexpr int LDSB = XB0 + (W == 8 ? 8 * 32 * 4 : 0);
+    __shared__ __attribute__((aligned(16))) char smem[LDSB];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+    const int qg = wave_s & 3, rh = wave_s >> 2;
     const int r32 = lane & 31, h = lane >> 5;
     const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;
     // long splits first (split-major dispatch, knn_engine.c: choose_splits)
@@ -133,21 +210,24 @@ __global__ __launch_bounds__(256, WPS) void k_dist_topk_i8(
     const int t_lo = split * tb + (split < tr ? split : tr);
     const int t_hi = t_lo + tb + (split < tr ? 1 : 0);
     const int qrow0 = qb * 128;
-    const int myq = qrow0 + 32 * wave + r32;
+    const int myq = qrow0 + 32 * qg + r32;
     const long gq = (long)q_base + myq;
-    const int nch = (nks + 3) >> 2;
+    constexpr int NCH = (NKS + 3) / 4;      // chunks a tile
+    const int nch = NCH;
     const int *qnorms = (const int *)(qsh + q_rows_pad * (size_t)rs);
     const int *cnorms = (const int *)(csh + c_rows_pad * (size_t)rs);
 
     // ---- resident query fragments (B), one per K-step --------------------
-    // (address clamped to the last real K-step: never past the row's block)
-    knn_v4i qf[4 * NC];
+    // NKS >= nks K-steps (the instantiation's bucket): those past nks get
+    // zero fragments, so the (garbage) corpus bytes they meet add nothing.
+    knn_v4i qf[NKS];
     {
         const signed char *qrow = qsh + (size_t)myq * rs + 16 * h;
 #pragma unroll
-        for (int s = 0; s < 4 * NC; s++) {
+        for (int s = 0; s < NKS; s++) {
             const int sl = s < nks ? s : nks - 1;
-            qf[s] = *(const knn_v4i *)(qrow + 32 * sl);
+            const knn_v4i v = *(const knn_v4i *)(qrow + 32 * sl);
+            qf[s] = s < nks ? v : (knn_v4i){0, 0, 0, 0};
         }
     }
     const int qn = qnorms[i8_norm_pos(myq)];
@@ -159,33 +239,47 @@ __global__ __launch_bounds__(256, WPS) void k_dist_topk_i8(
         const double td = __longlong_as_double((long long)atomicMin(qthr + myq, 0x7ff0000000000000ull));
         thr = td >= 2147483647.0 ? I8_INF : (int)td;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // vmcnt(0) through the builtin: hipcc's wait pass then knows the query
+    // loads are complete (an asm wait would leave it inserting vmcnt(N)
+    // before each later use of qf, draining the LDS-DMA ring)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
 
     int L[KL], I[KL];
 #pragma unroll
     for (int e = 0; e < KL; e++) { L[e] = I8_INF; I[e] = -1; }
-    const int ujm = uj < KL - 1 ? uj : KL - 1;
+    // uj: list slot of the 2-lane bound (low byte) and of the 4-lane bound
+    // (W = 8: the query's lanes in both waves; second byte)
+    const int ujm = (uj & 255) < KL - 1 ? (uj & 255) : KL - 1;
+    const int uj4 = (uj >> 8) < KL - 1 ? (uj >> 8) : KL - 1;
+    LDS_AS int *xb = (LDS_AS int *)(smem + XB0);
+    LDS_AS int *bk = (LDS_AS int *)(smem + BUF0) + wave_s * NB * 64 + lane;   // entry e at bk[64 e]
+    LDS_AS int *bi = bk + W * NB * 64;
+    int cnt = 0;   // buffered survivors of this lane
+    if constexpr (W == 8) {
+        if (h == 0) xb[wave_s * 32 + r32] = I8_INF;
+        __syncthreads();
+    }
 
-    // ---- staging cursor ----------------------------------------------------
+    // ---- staging ---------------------------------------------------------
     const int total = (t_hi > t_lo) ? (t_hi - t_lo) * nch : 0;
-    unsigned voff[4];
+    unsigned voff[PW];
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-        const int rr = 32 * wave_s + 8 * p + (lane >> 3);
+    for (int p = 0; p < PW; p++) {
+        const int rr = (128 / W) * wave_s + 8 * p + (lane >> 3);
         voff[p] = (unsigned)(rr * rs + 16 * ((lane & 7) ^ ((rr >> 1) & 7)));
     }
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
     int s_t = t_lo, s_c = 0, s_x = 0;
     auto stage = [&]() {
+        if constexpr ((ABL & 4) != 0) { s_x++; return; }
         const signed char *base = csh + (size_t)s_t * 128 * rs + 128 * s_c;
-        const knn_v4i rsrc = knn_rsrc(base);
-        const unsigned dst = lds0 + (unsigned)(s_x & (NST - 1)) * 16384u + (unsigned)wave_s * 4096u;
-#pragma unroll
-        for (int p = 0; p < 4; p++) bglds16(rsrc, voff[p], dst + 1024u * p);
+        const unsigned dst = lds0 + (unsigned)(s_x % NST) * 16384u + (unsigned)wave_s * (16384u / W);
+        if constexpr (PW == 4) bglds16x4(knn_rsrc(base), voff[0], voff[1], voff[2], voff[3], dst);
+        else bglds16x2(knn_rsrc(base), voff[0], voff[1], dst);
         if (s_x < total && s_c == 0) {
-            if (lane < 8)
-                bglds16(knn_rsrc(cnorms + (size_t)s_t * 128 + 32 * wave_s), 16u * lane,
-                        lds0 + NST * 16384u + (unsigned)(s_t & (NST - 1)) * 512u + 128u * wave_s);
+            if (lane < 32 / W)
+                bglds16(knn_rsrc(cnorms + (size_t)s_t * 128 + (128 / W) * wave_s), 16u * lane,
+                        lds0 + NORM0 + (unsigned)(s_t % NST) * 512u + (512u / W) * wave_s);
         }
         s_x++;
         if (s_x < total) {
@@ -195,16 +289,78 @@ __global__ __launch_bounds__(256, WPS) void k_dist_topk_i8(
             }
         }
     };
+    // the next chunk's own pieces landed: the NST - 3 chunks staged after it
+    // may stay in flight
+    auto wait_next = [&]() {
+        if constexpr ((ABL & 8) != 0) return;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (NST - 3)) : "memory");
+    };
+    // A fragments (MB m-blocks) of K-step ks of staged chunk xx
+    auto rdA = [&](int xx, int ks, knn_v4i (&a)[MB]) {
+        const LDS_AS char *p = (const LDS_AS char *)smem + (xx % NST) * 16384 + (MB * rh * 32 + r32) * 128 +
+                               16 * ((2 * ks + h) ^ ((r32 >> 1) & 7));
+#pragma unroll
+        for (int bb = 0; bb < MB; bb++) a[bb] = *(const LDS_AS knn_v4i *)(p + bb * 4096);
+    };
 
-    // ---- epilogue of tile t -------------------------------------------------
-    auto epilogue = [&](int t, knn_v16i (&A)[4]) {
+    // ---- bounds ------------------------------------------------------------------
+    // The bound a lane filters with: every value is an upper bound on the
+    // query's (k+1)-th smallest d^2 over all rows (or the lane's own KL-th,
+    // which it rejects anyway).  The wave's 2 lanes hold >= 2(ujm+1) >= k+1
+    // entries <= max_h L_h[ujm].  W = 8: the 4 lanes of both waves hold >=
+    // 4(uj4+1) >= k+1 entries <= the max of their L[uj4]; the partner wave's
+    // half comes through LDS, lock-free -- a stale value is larger (lists
+    // only shrink), so the max stays a valid bound, only a looser one.
+    auto refresh = [&]() {
+        int lmin = L[KL - 1], u = L[0], u4 = L[0];
+#pragma unroll
+        for (int e = 1; e < KL; e++) {
+            u = (e == ujm) ? L[e] : u;
+            u4 = (e == uj4) ? L[e] : u4;
+        }
+        const int lo = __shfl_xor(lmin, 32), uo = __shfl_xor(u, 32), u4o = __shfl_xor(u4, 32);
+        lmin = lo < lmin ? lo : lmin;
+        u = uo > u ? uo : u;
+        u4 = u4o > u4 ? u4o : u4;
+        int nb = lmin < u ? lmin : u;
+        if constexpr (W == 8) {
+            if (h == 0) xb[wave_s * 32 + r32] = u4;
+            const int pu = xb[(wave_s ^ 4) * 32 + r32];
+            u4 = pu > u4 ? pu : u4;
+            nb = u4 < nb ? u4 : nb;
+        }
+        thr = nb < thr ? nb : thr;
+    };
+    // buffered survivors -> lists, in buffer (= row) order, one entry a
+    // round; the rounds are dense: a merge runs when some lane's buffer is
+    // full, so most lanes insert a real entry every round
+    auto merge = [&]() {
+        for (int e = 0; __ballot(e < cnt) != 0ull; e++) {
+            int d = I8_INF, id = -1;
+            if (e < cnt) {
+                d = bk[64 * e];
+                id = bi[64 * e];
+                d = d > 0 ? d : I8_INF;   // d^2 == 0: an exact duplicate (serial:86)
+            }
+            i8_insert<KL>(L, I, d, id);
+        }
+        cnt = 0;
+        refresh();
+    };
+
+    // ---- epilogue of tile t --------------------------------------------------
+    auto epilogue = [&](int t, knn_v16i (&A)[MB]) {
+        if constexpr ((ABL & 1) != 0) {
+            L[0] = min(L[0], A[0][0] ^ A[MB - 1][3]);
+            return;
+        }
         const LDS_AS knn_v4i *cn =
-            (const LDS_AS knn_v4i *)((LDS_AS char *)smem + NST * 16384 + (t & (NST - 1)) * 512) + 4 * h;
+            (const LDS_AS knn_v4i *)((LDS_AS char *)smem + NORM0 + (t % NST) * 512) + 4 * h + 8 * MB * rh;
         const int lim = L[KL - 1] < thr ? L[KL - 1] : thr;
         const int limq = lim == I8_INF ? I8_INF : lim - qn;
         int lmn = I8_INF;
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
+        for (int b = 0; b < MB; b++) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const knn_v4i c4 = cn[8 * b + j];
@@ -216,100 +372,119 @@ __global__ __launch_bounds__(256, WPS) void k_dist_topk_i8(
                 }
             }
         }
-        const int row0 = t * 128;
-        const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 32 * wave_s;
-        const bool masked = (row0 + 128 > nc) || (gw0 < gt0 + 128 && gt0 < gw0 + 32);
+        const int row0 = t * 128 + 32 * MB * rh;
+        const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 32 * qg;
+        const bool masked = (row0 + 32 * MB > nc) || (gw0 < gt0 + 32 * MB && gt0 < gw0 + 32);
         if (!masked && __ballot(lmn <= limq) == 0ull) return;   // common late in the scan
+        if constexpr ((ABL & 2) != 0) {
+            L[0] = min(L[0], lmn);
+            return;
+        }
+        if constexpr ((ABL & 32) != 0) {
+            if (lane == 0) atomicAdd(&i8_dbg[0], 1ull);
+        }
+        const int idb = (int)(c_base + row0) + 4 * h;
+        // survivors of G m-blocks at a time (W = 8: both, one 32-bit mask):
+        // one wave round per survivor of the busiest lane; each lane takes its
+        // lowest pending candidate (lowest row: the stable tie order) through
+        // a select tree -- v_cndmask on ballot masks (as plain selects LLVM
+        // folds the tree into a dynamic index: a scratch round trip) -- into
+        // the KL-entry insertion network
+        constexpr int G = W == 8 ? 2 : 1;
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
+        for (int g0 = 0; g0 < MB; g0 += G) {
             unsigned pend = 0;
 #pragma unroll
-            for (int r = 0; r < 16; r++) pend |= (A[b][r] <= limq) ? (1u << r) : 0u;
+            for (int x = 0; x < 16 * G; x++) pend |= (A[g0 + (x >> 4)][x & 15] <= limq) ? (1u << x) : 0u;
             if (masked) {
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int row = row0 + 32 * b + 8 * (r >> 2) + 4 * h + (r & 3);
-                    if (!(row < nc && (long)c_base + row != gq)) pend &= ~(1u << r);
+                for (int x = 0; x < 16 * G; x++) {
+                    const int r = x & 15, rloc = 32 * (g0 + (x >> 4)) + 8 * (r >> 2) + (r & 3);
+                    if (!(row0 + rloc + 4 * h < nc && idb + rloc != gq)) pend &= ~(1u << x);
                 }
             }
             while (__ballot(pend != 0) != 0ull) {
-                const int r = pend ? __builtin_ctz(pend) : 0;
-                // 4-level select tree on the bits of r, written as v_cndmask
-                // on ballot masks: as plain selects LLVM folds the tree into a
-                // dynamic index (a scratch round trip per round)
-                const unsigned long long m0 = __ballot(r & 1), m1 = __ballot(r & 2),
-                                         m2 = __ballot(r & 4), m3 = __ballot(r & 8);
-                int v[8], w[4];
+                const int x = pend ? __builtin_ctz(pend) : 0;
+                int v[8 * G];
+                {
+                    const unsigned long long m0 = __ballot(x & 1);
 #pragma unroll
-                for (int y = 0; y < 8; y++) v[y] = i8_sel(m0, A[b][2 * y], A[b][2 * y + 1]);
+                    for (int y = 0; y < 8 * G; y++)
+                        v[y] = i8_sel(m0, A[g0 + (y >> 3)][(2 * y) & 15], A[g0 + (y >> 3)][(2 * y + 1) & 15]);
+                }
 #pragma unroll
-                for (int y = 0; y < 4; y++) w[y] = i8_sel(m1, v[2 * y], v[2 * y + 1]);
-                const int x0 = i8_sel(m2, w[0], w[1]), x1 = i8_sel(m2, w[2], w[3]);
-                const int d2 = i8_sel(m3, x0, x1) + qn;
-                // d^2 == 0: an exact duplicate (S == 0, excluded by serial:86)
-                const int dd = (pend && d2 > 0) ? d2 : I8_INF;
-                const int id = (int)(c_base + row0 + 32 * b + 8 * (r >> 2) + 4 * h + (r & 3));
+                for (int lv = 1, wdt = 8 * G; wdt > 1; lv++, wdt >>= 1) {
+                    const unsigned long long ml = __ballot((x >> lv) & 1);
+#pragma unroll
+                    for (int y = 0; y < wdt / 2; y++) v[y] = i8_sel(ml, v[2 * y], v[2 * y + 1]);
+                }
+                if (pend) {
+                    const int r = x & 15;
+                    bk[64 * cnt] = v[0] + qn;
+                    bi[64 * cnt] = idb + 32 * (g0 + (x >> 4)) + 8 * (r >> 2) + (r & 3);
+                    cnt++;
+                }
                 pend &= pend - 1;
-                list_insert<KL>(L, I, dd, id);
+                if constexpr ((ABL & 32) != 0) {
+                    if (lane == 0) atomicAdd(&i8_dbg[1], 1ull);
+                }
+                if (__ballot(cnt == NB) != 0ull) merge();
             }
         }
-        // bound shared by the query's 2 lanes: their union holds >= 2(ujm+1)
-        // >= k+1 entries <= max_h L_h[ujm]; each already rejects >= its L[KL-1]
-        int lmin = L[KL - 1], u = L[0];
-#pragma unroll
-        for (int e = 1; e < KL; e++) u = (e == ujm) ? L[e] : u;
-        const int lo = __shfl_xor(lmin, 32), uo = __shfl_xor(u, 32);
-        lmin = lo < lmin ? lo : lmin;
-        u = uo > u ? uo : u;
-        const int nb = lmin < u ? lmin : u;
-        thr = nb < thr ? nb : thr;
     };
 
+    // ---- main loop -------------------------------------------------------------
     if (total > 0) {
 #pragma unroll
-        for (int x = 0; x < NST - 1; x++) stage();
+        for (int y = 0; y < NST - 2; y++) stage();
+        wait_next();
+        __builtin_amdgcn_s_barrier();
+        knn_v4i acur[MB], anxt[MB];
+        rdA(0, 0, acur);
+        stage();
         int x = 0;
         for (int t = t_lo; t < t_hi; t++) {
-            knn_v16i acc[4];
+            knn_v16i acc[MB];
 #pragma unroll
-            for (int b = 0; b < 4; b++)
+            for (int bb = 0; bb < MB; bb++)
 #pragma unroll
-                for (int i = 0; i < 16; i++) acc[b][i] = 0;
+                for (int i = 0; i < 16; i++) acc[bb][i] = 0;
 #pragma unroll
-            for (int c = 0; c < NC; c++) {
-                if (c < nch) {
-                    // own pieces of chunk x landed (those of the next NST-2
-                    // chunks may stay in flight); then every wave's
-                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                    __builtin_amdgcn_s_barrier();
-                    stage();   // chunk x + NST - 1 into the stage chunk x - 1 freed
-                    const LDS_AS char *st = (const LDS_AS char *)smem + (x & (NST - 1)) * 16384 +
-                                            r32 * 128;
+            for (int c = 0; c < NCH; c++) {
+                const int kt = NKS - 4 * c < 4 ? NKS - 4 * c : 4;   // static after unrolling
 #pragma unroll
-                    for (int s = 0; s < 4; s++) {
-                        if (4 * c + s < nks) {
-                            const int slot = 16 * ((2 * s + h) ^ ((r32 >> 1) & 7));
-                            knn_v4i a[4];
-#pragma unroll
-                            for (int b = 0; b < 4; b++)
-                                a[b] = *(const LDS_AS knn_v4i *)(st + b * 4096 + slot);
-#pragma unroll
-                            for (int b = 0; b < 4; b++)
-                                acc[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[b], qf[4 * c + s], acc[b], 0,
-                                                                               0, 0);
+                for (int ks = 0; ks < 4; ks++) {
+                    if (ks < kt) {
+                        if (ks + 1 < kt) {
+                            rdA(x, ks + 1, anxt);
+                        } else if (x + 1 < total) {
+                            wait_next();
+                            if constexpr ((ABL & 8) == 0) __builtin_amdgcn_s_barrier();   // B(x + 1)
+                            rdA(x + 1, 0, anxt);
+                            stage();
                         }
+                        if constexpr ((ABL & 16) == 0) {
+#pragma unroll
+                            for (int bb = 0; bb < MB; bb++)
+                                acc[bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(acur[bb], qf[4 * c + ks],
+                                                                                acc[bb], 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int bb = 0; bb < MB; bb++) acur[bb] = anxt[bb];
                     }
-                    x++;
                 }
+                x++;
             }
             epilogue(t, acc);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA left in flight
     }
+    merge();
 
     // strict publication (INT mode, exact keys): if neither lane's list ends
     // at thr, nothing equal to thr was turned away, so every rejected
-    // candidate has d^2 >= next(thr) (k_finalize certifies tau < T)
+    // candidate has d^2 >= next(thr) (k_finalize certifies tau < T); W = 8:
+    // T of the query = min over its two waves (LDS, after a barrier)
     int lastmin = L[KL - 1];
     {
         const int o = __shfl_xor(lastmin, 32);
@@ -317,18 +492,26 @@ __global__ __launch_bounds__(256, WPS) void k_dist_topk_i8(
     }
     double pub = thr == I8_INF ? KNN_INF : (double)thr;
     if (lastmin > thr && thr < I8_INF) pub = nextafter((double)thr, KNN_INF);
+    if constexpr (W == 8) {
+        double *xd = (double *)((char *)smem + NORM0);   // the norm ring is free now
+        __syncthreads();
+        if (h == 0 && rh == 1) xd[qg * 32 + r32] = pub;
+        __syncthreads();
+        if (rh == 0) {
+            const double po = xd[qg * 32 + r32];
+            pub = po < pub ? po : pub;
+        }
+    }
     if (myq < nq) {
-        const size_t base = (((size_t)split * nq_pad + myq) * 2 + h) * KL;
+        const size_t base = (((size_t)split * nq_pad + myq) * LPQ + 2 * rh + h) * KL;
 #pragma unroll
         for (int e = 0; e < KL; e++) {
             part_d[base + e] = L[e] == I8_INF ? KNN_INF : (double)L[e];
             part_i[base + e] = I[e];
         }
-        if (h == 0) {
-            part_T[(size_t)split * nq_pad + myq] = pub;
-            if (qthr != nullptr && thr < I8_INF)
-                atomicMin(qthr + myq, (unsigned long long)__double_as_longlong((double)thr));
-        }
+        if (h == 0 && rh == 0) part_T[(size_t)split * nq_pad + myq] = pub;
+        if (h == 0 && qthr != nullptr && thr < I8_INF)
+            atomicMin(qthr + myq, (unsigned long long)__double_as_longlong((double)thr));
     }
 }
 
@@ -352,13 +535,13 @@ extern "C" int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t 
     return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
 }
 
-template <int KL, int NC, int WPS>
+template <int KL, int NKS, int W, int WPS, int NST, int NB>
 static void launch_i8(dim3 grid, hipStream_t s, const void *qsh, size_t q_rows_pad, size_t q_base,
                       int nq, const void *csh, size_t c_rows_pad, size_t c_base, int nc, int rs,
                       int nks, int ntiles, int nsplit, int nqb, double *part_d, int *part_i,
                       double *part_T, int nq_pad, double *qthr, int uj)
 {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KL, NC, WPS>), grid, dim3(256), 0, s,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KL, NKS, W, WPS, NST, NB>), grid, dim3(64 * W), 0, s,
                        (const signed char *)qsh, q_rows_pad, q_base, nq, (const signed char *)csh,
                        c_rows_pad, c_base, nc, rs, nks, ntiles, nsplit, nqb, part_d, part_i, part_T,
                        nq_pad, (unsigned long long *)qthr, uj);
@@ -369,25 +552,34 @@ extern "C" int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_
                                   int n, int nsplit, double *part_d, int *part_i, double *part_T,
                                   int nq_pad, double *qthr, void *stream)
 {
-    const int rs = (int)knn_s8_rs((size_t)n), nks = rs / 32, nch = (nks + 3) / 4;
+    const int rs = (int)knn_s8_rs((size_t)n), nks = rs / 32;
     const int nqb = (nq + 127) / 128, ntiles = (nc + 127) / 128;
     const int kl = knn_i8_kl(kp);
-    if (nqb <= 0 || nsplit <= 0 || k <= 0 || k > kp || kl <= 0 || nch > 7) return KNN_ERR_INVALID;
+    if (nqb <= 0 || nsplit <= 0 || k <= 0 || k > kp || kl <= 0 || nks > 28) return KNN_ERR_INVALID;
     if ((size_t)nqb * 128 > q_rows_pad || (size_t)ntiles * 128 > c_rows_pad || nq_pad < nqb * 128)
         return KNN_ERR_INVALID;
     // lane-list slot of the shared bound: the 2 lanes of a query cover k + 1
-    int uj = (k + 1 + 1) / 2 - 1;
+    int uj = (k + 1 + 1) / 2 - 1, uj4 = (k + 1 + 3) / 4 - 1;
     if (uj > kl - 1) uj = kl - 1;
+    uj |= uj4 << 8;
     const dim3 grid((unsigned)(nqb * nsplit));
     hipStream_t s = (hipStream_t)stream;
 #define I8_ARGS grid, s, qsh, q_rows_pad, q_base, nq, csh, c_rows_pad, c_base, nc, rs, nks, ntiles, nsplit, \
                 nqb, part_d, part_i, part_T, nq_pad, qthr, uj
-    if (nch == 1) {
-        if (kl == KNN_I8_KL) launch_i8<KNN_I8_KL, 1, 2>(I8_ARGS);
-        else launch_i8<KNN_I8_KL_L, 1, 1>(I8_ARGS);
+    // one chunk a tile (n <= 128): two workgroups a CU, 4-stage rings;
+    // else one workgroup a CU (queries in up to 112 VGPRs), 8 stages
+    // k <= 32: 8 waves (two a SIMD, 2 m-blocks each, 4 lists a query);
+    // k <= 128: 4 waves (one a SIMD, 4 m-blocks, 2 lists a query, 512 VGPRs).
+    // K-step buckets: the smallest instantiated NKS >= nks
+    if (kl == KNN_I8_KL) {
+        if (nks <= 4) launch_i8<KNN_I8_KL, 4, 8, 2, 7, 8>(I8_ARGS);
+        else if (nks <= 8) launch_i8<KNN_I8_KL, 8, 8, 2, 7, 8>(I8_ARGS);
+        else if (nks <= 16) launch_i8<KNN_I8_KL, 16, 8, 2, 7, 8>(I8_ARGS);
+        else if (nks <= 25) launch_i8<KNN_I8_KL, 25, 8, 2, 7, 8>(I8_ARGS);
+        else launch_i8<KNN_I8_KL, 28, 8, 2, 7, 8>(I8_ARGS);
     } else {
-        if (kl == KNN_I8_KL) launch_i8<KNN_I8_KL, 7, 1>(I8_ARGS);
-        else launch_i8<KNN_I8_KL_L, 7, 1>(I8_ARGS);
+        if (nks <= 4) launch_i8<KNN_I8_KL_L, 4, 4, 1, 8, 8>(I8_ARGS);
+        else launch_i8<KNN_I8_KL_L, 28, 4, 1, 8, 8>(I8_ARGS);
     }
 #undef I8_ARGS
     return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;

@@ -67,12 +67,13 @@ static inline int knn_rescan_chunks(int nfail)
 static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
 
 /* Byte block (knn_i8.hip): the int8 form of a packed block for the int8
- * MFMA contraction of 8-bit-window integer data.  Rows of round_up(n, 32)
- * bytes (x - o, o = 128 - meta[MAXNEG]), then one int32 |x - o|^2 per row in
+ * MFMA contraction of 8-bit-window integer data.  Rows of knn_s8_rs(n)
+ * bytes (x - o, o = 128 - meta[MAXNEG]; 0 past n), then one int32 |x - o|^2 per row in
  * the per-tile order of i8_norm_pos, then the block's 8 meta doubles. */
 #define KNN_I8_MAX_N 896  /* 7 chunks of 128 features: queries stay in VGPRs */
-#define KNN_I8_KL   24    /* per-lane list length, k <= 32 (2 lanes a query) */
-#define KNN_I8_KL_L 48    /* k <= 128                                         */
+#define KNN_I8_KL   17    /* per-lane list, k <= 32: 8-wave kernel, 4 lists a query  */
+#define KNN_I8_KL_L 65    /* k <= 128: 4-wave kernel, 2 lists a query (2 KL > k)    */
+/* row bytes: whole K-steps of 32 */
 static inline size_t knn_s8_rs(size_t n) { return knn_round_up(n ? n : 1, 32); }
 static inline size_t knn_s8_norm_offset(size_t cap, size_t n) { return knn_rows_pad(cap) * knn_s8_rs(n); }
 static inline size_t knn_s8_bytes(size_t cap, size_t n)
@@ -80,6 +81,7 @@ static inline size_t knn_s8_bytes(size_t cap, size_t n)
     return knn_round_up(knn_s8_norm_offset(cap, n) + knn_rows_pad(cap) * 4 + 8 * sizeof(double), 16);
 }
 static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL : KNN_I8_KL_L; }
+static inline int knn_i8_lpq(int kp) { return kp <= KNN_KP_M ? 4 : 2; }
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
 {
     return knn_round_up(n ? n : 1, 128 / knn_esize(dtype));

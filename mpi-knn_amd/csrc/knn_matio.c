@@ -89,9 +89,21 @@ static int parse_matrix(const uint8_t *p, size_t n, int swap, mx_t *mx, int head
     off = next;
     if (read_tag(&b, off, &t, &nb, &d, &next) || t != miINT32 || nb < 4) return KNN_ERR_FORMAT;
     mx->ndims = (int)(nb / 4);
-    mx->dims[0] = (int32_t)rd32(d, swap);
-    mx->dims[1] = mx->ndims > 1 ? (int32_t)rd32(d + 4, swap) : 1;
-    for (int i = 2; i < mx->ndims; i++) mx->dims[1] *= (int32_t)rd32(d + 4 * i, swap);
+    /* dims are non-negative and their product must not wrap: trailing dims
+     * fold into dims[1] in 64-bit, capped at INT32_MAX each */
+    {
+        const int32_t d0 = (int32_t)rd32(d, swap);
+        int64_t d1 = mx->ndims > 1 ? (int32_t)rd32(d + 4, swap) : 1;
+        if (d0 < 0 || d1 < 0) return KNN_ERR_FORMAT;
+        for (int i = 2; i < mx->ndims; i++) {
+            const int32_t di = (int32_t)rd32(d + 4 * i, swap);
+            if (di < 0) return KNN_ERR_FORMAT;
+            d1 *= di;
+            if (d1 > INT32_MAX) return KNN_ERR_FORMAT;
+        }
+        mx->dims[0] = d0;
+        mx->dims[1] = (int32_t)d1;
+    }
     off = next;
     if (read_tag(&b, off, &t, &nb, &d, &next) || (t != miINT8 && t != miUTF8)) return KNN_ERR_FORMAT;
     size_t ln = nb < sizeof(mx->name) - 1 ? nb : sizeof(mx->name) - 1;
@@ -142,8 +154,12 @@ static int to_double(const mx_t *mx, int swap, double **out, size_t *count)
 {
     const int sz = elem_size(mx->re_type);
     if (!sz) return KNN_ERR_FORMAT;
-    const size_t cnt = (size_t)(mx->dims[0] < 0 ? 0 : mx->dims[0]) * (size_t)(mx->dims[1] < 0 ? 0 : mx->dims[1]);
-    if ((size_t)mx->re_bytes < cnt * (size_t)sz) return KNN_ERR_FORMAT;
+    if (mx->dims[0] < 0 || mx->dims[1] < 0) return KNN_ERR_FORMAT;
+    const uint64_t cnt64 = (uint64_t)mx->dims[0] * (uint64_t)mx->dims[1];   /* < 2^62 */
+    /* the payload must hold cnt elements: compare by division, no wrap */
+    if (cnt64 > (uint64_t)mx->re_bytes / (uint64_t)sz || cnt64 > SIZE_MAX / sizeof(double))
+        return KNN_ERR_FORMAT;
+    const size_t cnt = (size_t)cnt64;
     double *v = (double *)malloc((cnt ? cnt : 1) * sizeof(double));
     if (!v) return KNN_ERR_NOMEM;
     if (mx->re_type == miDOUBLE && !swap) {

@@ -63,3 +63,20 @@ def test_no_labels_variable_ok(knn, tmp_path):
     scipy.io.savemat(path, {"train_X": np.arange(12.0).reshape(3, 4)})
     X, lab = knn.load_mat(path, lvar=None)
     assert lab is None and np.array_equal(X, np.arange(12.0).reshape(3, 4))
+
+
+@pytest.mark.parametrize("dims", [(0x7fffffff, 0x7fffffff), (-5, 3), (5, -3), (0x40000000, 8)])
+def test_malformed_dims_rejected(knn, tmp_path, dims):
+    """Crafted dims must fail cleanly (KNN_ERR_FORMAT), never size a buffer
+    from a wrapped product: 8-byte classes, negative and huge dims."""
+    path = tmp_path / "crafted.mat"
+    X = np.arange(15, dtype=np.int64).reshape(5, 3)
+    scipy.io.savemat(str(path), {"train_X": X}, do_compression=False)
+    raw = bytearray(path.read_bytes())
+    at = raw.find(np.array([5, 3], dtype="<i4").tobytes())
+    assert at > 0
+    raw[at:at + 8] = np.array(dims, dtype="<i4").tobytes()
+    path.write_bytes(bytes(raw))
+    with pytest.raises(knn.KnnError) as e:
+        knn.load_mat(str(path), lvar=None)
+    assert e.value.status == knn.ERR_FORMAT

@@ -1,0 +1,81 @@
+"""Drive tools/probe/kbench8 (k_dist_topk_i8 ablations) on real engine data.
+
+  python tools/probe/kbench8.py [--workload mnist|sift] [--iters 5] [--abl 0,1,2,...]
+
+ABL bits (k_dist_topk_i8's tuning argument): 1 no epilogue, 2 epilogue
+keys + lane minimum only (no insertion), 4 no staging DMA (garbage data),
+8 no chunk wait/barrier (racy), 16 no MFMA.  Variant 0 is the product
+kernel.  Prints one JSON line per variant."""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "mpi-knn_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="mnist")
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--splits", type=int, default=0)
+    ap.add_argument("--abl", default="0,1,2,4,8,16")
+    a = ap.parse_args()
+    so = os.path.join(HERE, "libkbench8.so")
+    if not os.path.exists(so):
+        raise SystemExit("build first: make -C tools/probe kbench8")
+    import torch
+    import mpiknn
+    import mpiknn.ring as ring
+    from mpiknn import synth
+    if a.workload == "mnist":
+        X, _ = synth.mnist_like(60000, 784)
+        k, dt, splits = 30, "f64", 6
+    else:
+        X = synth.sift_like(1000000, 128)
+        k, dt, splits = 32, "f32", 3
+    splits = a.splits or splits
+    m, n = X.shape
+    eng = ring.GpuEngine(torch, 0, n, m, m, k, dtype=dt)
+    eng.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
+    eng.begin(0)
+    assert eng.ctx.shadow() == 2, "data not int8-eligible"
+    sb = torch.empty(eng.ctx.shadow_bytes(m), dtype=torch.uint8, device="cuda:0")
+    eng.ctx.shadow_pack(sb.data_ptr(), eng.qb.data_ptr(), m, eng.stream())
+    torch.cuda.synchronize()
+    nq_pad = (m + 127) // 128 * 128
+    rp = nq_pad
+    kl = 17   # KNN_I8_KL, 4 lists a query
+    pd = torch.empty(splits * nq_pad * 4 * kl, dtype=torch.float64, device="cuda:0")
+    pi = torch.empty(splits * nq_pad * 4 * kl, dtype=torch.int32, device="cuda:0")
+    pT = torch.empty(splits * nq_pad, dtype=torch.float64, device="cuda:0")
+    qthr = torch.empty(nq_pad, dtype=torch.float64, device="cuda:0")
+    L = ctypes.CDLL(so)
+    p, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    L.kbench8.argtypes = [i, p, sz, i, p, sz, i, i, i, i, p, p, p, i, p, i]
+    L.kbench8.restype = ctypes.c_float
+    flop = 2.0 * m * m * n
+    cnt = (ctypes.c_ulonglong * 4)()
+    for abl in [int(x) for x in a.abl.split(",")]:
+        L.kbench8_reset()
+        ms = L.kbench8(abl, sb.data_ptr(), rp, m, sb.data_ptr(), rp, m, n, k, splits,
+                       pd.data_ptr(), pi.data_ptr(), pT.data_ptr(), nq_pad, qthr.data_ptr(), a.iters)
+        rec = {"workload": a.workload, "abl": abl, "splits": splits, "ms": ms,
+               "tops": flop / (ms * 1e-3) / 1e12 if ms > 0 else None}
+        if abl & 32:
+            L.kbench8_counters(cnt)
+            runs = a.iters + 1
+            wave_tiles = (m // 128 + 1) * splits * 8 * ((m // 128 + 1) // splits)
+            rec.update(survivor_wave_tiles=cnt[0] / runs, rounds=cnt[1] / runs,
+                       wave_tiles_approx=wave_tiles)
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
