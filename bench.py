@@ -10,12 +10,14 @@ full all-kNN pass with the corpus already resident in HBM (column-major, the
 block) -> finalize (+ exact rescan if any query needs it).
 value = m / step time (whole job).
 
+--workload mnist-real: the same shape real-valued (mnist_like / 255 + N(0,
+1e-3)), so the fp64 GEMM mode runs: v_mfma_f64 filter + exact re-rank.
 --workload sift: configs[3], 1M x 128 fp32 k = 32 (SIFT-like integers,
 row-major fvecs layout).  --workload gist: configs[4]'s shape, n = 960 fp32
 k = 100, with m = 500000 by default (configs[4] is 4M rows on 8 GPUs; pass
 --m 4000000 for the full size).  Both run the fp32 path (include/knn.h).
 
-  python bench.py [--gpus N --steps K --warmup W] [--workload mnist|sift|gist]
+  python bench.py [--gpus N --steps K --warmup W] [--workload mnist|mnist-real|sift|gist]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 N > 1: one process per GPU, RCCL (torch.distributed "nccl") ring of corpus
@@ -43,6 +45,10 @@ WORKLOADS = {
     # name: (m, n, k, dtype, layout_col, description)
     "mnist": (60000, 784, 30, "f64", True,
               "all-kNN MNIST-784 k=%d (configs[1]: %dx%d fp64, leave-one-out)"),
+    # configs[1] on real-valued rows (mnist_train_svd.mat is
+    # real-valued): GEMM mode, fp64 MFMA filter + exact re-rank in k_merge
+    "mnist-real": (60000, 784, 30, "f64", True,
+                   "all-kNN MNIST-784 real-valued k=%d (configs[1] shape: %dx%d fp64, GEMM mode)"),
     "sift": (1_000_000, 128, 32, "f32", False,
              "all-kNN SIFT-like k=%d (configs[3]: %dx%d fp32, integer-valued)"),
     "gist": (500_000, 960, 100, "f32", False,
@@ -107,6 +113,9 @@ def main():
     if args.workload == "mnist":
         X, _ = synth.mnist_like(m, n)
         data = "synthetic (MNIST-784 shape, integer pixels 0..255, seed 1234)"
+    elif args.workload == "mnist-real":
+        X, _ = synth.mnist_real(m, n)
+        data = "synthetic (MNIST-784 shape / 255 + N(0, 1e-3): real-valued fp64)"
     elif args.workload == "sift":
         X = synth.sift_like(m, n)
         data = "synthetic (SIFT-like: 1024-centre mixture, integers 0..255, fp32)"

@@ -28,6 +28,17 @@ def mnist_like(m=60000, n=784, seed=1234):
     return X, (y + 1).astype(np.float64)
 
 
+def mnist_real(m=60000, n=784, seed=1234, noise_seed=0x5EA1):
+    """The real-valued MNIST variant (mnist_train_svd.mat is
+    real-valued): mnist_like(m, n, seed) / 255 + N(0, 1e-3) (numpy
+    default_rng(noise_seed)), fp64.  Not integer, so the engine runs its
+    GEMM mode: fp64 MFMA filter + exact reference-order re-rank."""
+    X, y = mnist_like(m, n, seed)
+    X /= 255.0
+    X += np.random.default_rng(noise_seed).normal(0, 1e-3, X.shape)
+    return X, y
+
+
 def sift_like(m=1_000_000, n=128, clusters=1024, seed=0x51F7, chunk=1 << 18):
     """BASELINE.json configs[3] shape: SIFT-like 1M x 128, a mixture of
     `clusters` Gaussian centres clipped to [0, 255] and rounded (integer

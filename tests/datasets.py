@@ -42,6 +42,14 @@ def mnist_like(m, n=784, seed=1234):
     return X.astype(np.float64), (y + 1).astype(np.float64)
 
 
+def mnist_real(m, n=784, seed=1234, noise_seed=0x5EA1):
+    """Real-valued MNIST-shaped corpus (mpiknn.synth.mnist_real): the integer
+    corpus / 255 + N(0, 1e-3), fp64 -- the engine's GEMM mode."""
+    X, y = mnist_like(m, n, seed)
+    X = X / 255.0 + np.random.default_rng(noise_seed).normal(0, 1e-3, X.shape)
+    return X, y
+
+
 def sift_like(m, n=128, clusters=1024, seed=0x51F7):
     """BASELINE configs[3] shape (SIFT-like): Gaussian mixture of `clusters`
     centres, clipped to [0, 255] and rounded -- integer-valued, fp32."""

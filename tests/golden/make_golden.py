@@ -18,7 +18,12 @@ hold, so the GPU tests can check neighbour lists against committed data:
                       distances' raw fp64 bits (u64);
 * mnist_like_sample.npz  datasets.mnist_like(60000): 48 sampled queries
                       against the full 60000x784 corpus, k=30: rows, idx
-                      (i32), d2 (u32, exact integers).
+                      (i32), d2 (u32, exact integers);
+* mnist_real_sample.npz  datasets.mnist_real(60000) (real-valued, the GEMM
+                      mode): the same 48 rows, k=30: rows, idx (i32), the
+                      distances' raw fp64 bits (u64).
+
+  python tests/golden/make_golden.py [--only mnist_real]
 """
 import json
 import os
@@ -56,7 +61,23 @@ def mnist_sample_rows(m=60000, q=48):
     return np.concatenate([[0], rows, [m - 1]]).astype(np.int64)
 
 
+def mnist_real_fixture():
+    Xm, _ = datasets.mnist_real(60000)
+    rows = mnist_sample_rows()
+    idx = np.zeros((len(rows), 30), np.int32)
+    bits = np.zeros((len(rows), 30), np.uint64)
+    for i, r in enumerate(rows):
+        nb = oracle.knn(Xm, 30, rows=(int(r), 1))
+        idx[i] = nb["idx"][0]
+        bits[i] = nb["distance"][0].view(np.uint64)
+    np.savez_compressed(os.path.join(HERE, "mnist_real_sample.npz"), rows=rows, idx=idx,
+                        dist_bits=bits)
+
+
 def main():
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "mnist_real":
+        mnist_real_fixture()
+        return
     with open(os.path.join(HERE, "reference_runs.json"), "w") as f:
         json.dump(REFERENCE_RUNS, f, indent=1)
         f.write("\n")
@@ -87,6 +108,7 @@ def main():
         idx[i] = nb["idx"][0]
         d2[i] = exact_s(nb["distance"][0])
     np.savez_compressed(os.path.join(HERE, "mnist_like_sample.npz"), rows=rows, idx=idx, d2=d2)
+    mnist_real_fixture()
     print("golden fixtures written to", HERE)
 
 

@@ -4,7 +4,9 @@ CPU: the oracle reproduces the reference-run aggregates (reference_runs.json,
 SURVEY.md sec.0/sec.4) and the committed neighbour fixtures.  GPU: libknn
 through the C ABI reproduces the same fixtures bit for bit -- digits (integer
 mode), the real-valued digits variant (GEMM filter + exact re-rank) and 48
-sampled queries of the full 60000x784 MNIST-shaped corpus (configs[1]).
+sampled queries of the full 60000x784 MNIST-shaped corpus (configs[1]), in
+its integer form and its real-valued form (SURVEY C1's svd variant is
+real-valued: GEMM mode on fp64 MFMA plus the exact re-rank, at full size).
 """
 import json
 import os
@@ -118,3 +120,27 @@ def test_gpu_mnist_single_split_rescan(knn, monkeypatch):
     assert base.tobytes() == one.tobytes()
     g = load("mnist_like_sample.npz")
     check_mnist_rows(one[g["rows"]], g)
+
+
+def test_oracle_matches_mnist_real_sample(oracle):
+    g = load("mnist_real_sample.npz")
+    X, _ = datasets.mnist_real(60000)
+    rows = g["rows"][::12]
+    got = np.concatenate([oracle.knn(X, 30, rows=(int(r), 1)) for r in rows])
+    assert np.array_equal(got["idx"], g["idx"][::12])
+    assert np.array_equal(got["distance"].view(np.uint64), g["dist_bits"][::12])
+
+
+@pytest.mark.gpu
+def test_gpu_mnist_real_full_size_fixture(knn):
+    """The real-valued 60000x784 corpus at full size through the C ABI (fp64
+    GEMM mode: v_mfma_f64 filter, exact re-rank in k_merge, certificate):
+    the 48 committed rows bit-exact (indices and distance bits)."""
+    X, _ = datasets.mnist_real(60000)
+    nb, _ = knn.search(np.asfortranarray(X), 30, layout="col")
+    g = load("mnist_real_sample.npz")
+    got = nb[g["rows"]]
+    assert np.array_equal(got["idx"], g["idx"])
+    assert np.array_equal(got["distance"].view(np.uint64), g["dist_bits"])
+    d = nb["distance"]
+    assert np.all(d[:, 1:] >= d[:, :-1]) and np.all(d > 0)
