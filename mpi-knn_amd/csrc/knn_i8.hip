@@ -102,35 +102,49 @@ __device__ __forceinline__ int i8_sel(unsigned long long m, int a, int b)
     return r;
 }
 
-// One wave per row: x' = x - o (0 past n), 16 bytes a lane, |x'|^2 reduced
-// in int32 (exact: n * 128^2 < 2^31).  o from the REDUCED meta, so every
-// block of one search shifts alike.
+// One wave per row: x' = x - o (0 past n), |x'|^2 reduced in int32 (exact:
+// n 128^2 < 2^31).  Lane l converts the 8-element groups l, l + 64, ... of
+// the row: 16-byte vector loads (a wave reads 64 contiguous groups), one
+// 8-byte store.  o from the REDUCED meta, so every block of one search
+// shifts alike.
 template <typename T>
 __global__ __launch_bounds__(256) void k_shadow8(signed char *__restrict__ dst, const T *__restrict__ src,
                                                  size_t rows_pad, int n, int nps, int rs,
                                                  const double *__restrict__ meta)
 {
+    typedef typename std::conditional<sizeof(T) == 8, dbl2, flt4>::type vec_t;
+    constexpr int V = 16 / (int)sizeof(T);            // elements per 16-byte load
     int *norms = (int *)(dst + rows_pad * (size_t)rs);
     const int off = 128 - (int)meta[KNN_META_MAXNEG];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ng = rs / 8;                             // 8-byte output groups a row
     for (size_t r = (size_t)blockIdx.x * 4 + wave; r < rows_pad; r += (size_t)gridDim.x * 4) {
         const T *x = src + r * (size_t)nps;
         int s = 0;
-        for (int c0 = lane * 16; c0 < rs; c0 += 1024) {
-            unsigned w[4];
+        for (int g = lane; g < ng; g += 64) {
+            const int j0 = 8 * g;
+            T v[8];
+            if (j0 + 8 <= nps) {                        // whole group inside the padded row
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                unsigned word = 0;
+                for (int q = 0; q < 8 / V; q++) {
+                    const vec_t w = *(const vec_t *)(x + j0 + V * q);
 #pragma unroll
-                for (int y = 0; y < 4; y++) {
-                    const int j = c0 + 4 * e + y;
-                    const int v = j < n ? (int)x[j] - off : 0;
-                    s += v * v;
-                    word |= ((unsigned)v & 0xffu) << (8 * y);
+                    for (int e = 0; e < V; e++) v[V * q + e] = w[e];
                 }
-                w[e] = word;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++) v[e] = j0 + e < nps ? x[j0 + e] : (T)0;
             }
-            *(knn_v4i *)(dst + r * (size_t)rs + c0) = (knn_v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+            unsigned lo = 0, hi = 0;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const int xi = j0 + e < n ? (int)v[e] - off : 0;
+                s += xi * xi;
+                if (e < 4) lo |= ((unsigned)xi & 0xffu) << (8 * e);
+                else hi |= ((unsigned)xi & 0xffu) << (8 * (e - 4));
+            }
+            typedef unsigned u2 __attribute__((ext_vector_type(2)));
+            *(u2 *)(dst + r * (size_t)rs + j0) = (u2){lo, hi};
         }
         for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
         if (lane == 0) norms[i8_norm_pos((int)r)] = s;
@@ -522,7 +536,7 @@ extern "C" int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t 
                                   const double *meta, void *stream)
 {
     const int rs = (int)knn_s8_rs(n), nps = (int)knn_n_pad_dt(n, dtype);
-    const unsigned grid = (unsigned)(rows_pad / 4 + 1 < 8192 ? rows_pad / 4 + 1 : 8192);
+    const unsigned grid = (unsigned)((rows_pad + 3) / 4 < 4096 ? (rows_pad + 3) / 4 : 4096);
     hipStream_t s = (hipStream_t)stream;
     if (dtype == KNN_F64)
         hipLaunchKernelGGL(k_shadow8<double>, dim3(grid), dim3(256), 0, s, (signed char *)dst,

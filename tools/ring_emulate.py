@@ -2,12 +2,21 @@
 """One rank's share of a P-GPU ring, emulated on one GPU (diagnostic only).
 
 The scaling bench (N = 2/4/8 GPUs) is run by the driver; this tool measures
-what each rank computes there -- its R = ceil(m/P) query rows against the P
-corpus blocks, k_dist_topk + k_merge per block, then finalize -- with the
-blocks already resident (no RCCL hop), so that the compute-side strong-scaling
-efficiency t(1) / (P * t_rank(P)) can be read before an 8-GPU node runs it.
+what each rank computes there -- rank 0's R = ceil(m/P) query rows against
+the P corpus blocks, k_dist_topk + k_merge per block, then finalize -- with
+the blocks already resident in the form the ring moves (byte / fp16 shadow
+blocks when the search stages them, element blocks otherwise; no RCCL hop),
+so the compute-side strong-scaling efficiency t(1) / (P * t_rank(P)) can be
+read before an 8-GPU node runs it.
 
-  python tools/ring_emulate.py [--workload mnist] [--ranks 1,2,4,8] [--steps 3]
+  python tools/ring_emulate.py [--workload mnist|mnist-real|sift|gist]
+                               [--ranks 1,2,4,8] [--steps 3] [--m M]
+
+configs[3] (sift, 1M x 128 fp32, k = 32) and configs[4] (gist, 4M x 960 fp32,
+k = 100) are 8-GPU configurations: --ranks 8 gives their per-rank work
+(125K x 8 blocks of 125K rows; 500K x 8 blocks of 500K rows).  The gist-shaped
+corpus is generated on the device (a 256-centre mixture in [0, 1), like
+mpiknn.synth.gist_like) to keep 15 GB off the host.
 """
 import argparse
 import json
@@ -20,56 +29,83 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mpi-knn_amd"))
 
+WORKLOADS = {   # m, n, k, dtype
+    "mnist": (60000, 784, 30, "f64"),
+    "mnist-real": (60000, 784, 30, "f64"),
+    "sift": (1_000_000, 128, 32, "f32"),
+    "gist": (4_000_000, 960, 100, "f32"),
+}
+
+
+def corpus(torch, workload, m, n, dev):
+    from mpiknn import synth
+    if workload == "mnist":
+        return torch.from_numpy(synth.mnist_like(m, n)[0]).to(dev)
+    if workload == "mnist-real":
+        return torch.from_numpy(synth.mnist_real(m, n)[0]).to(dev)
+    if workload == "sift":
+        return torch.from_numpy(synth.sift_like(m, n)).to(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x6157)
+    centres = torch.rand((256, n), generator=g, device=dev) * 0.5 + 0.1
+    X = torch.empty((m, n), dtype=torch.float32, device=dev)
+    step = 1 << 18
+    for lo in range(0, m, step):
+        hi = min(m, lo + step)
+        lab = torch.randint(0, 256, (hi - lo,), generator=g, device=dev)
+        X[lo:hi] = (centres[lab] + 0.08 * torch.randn((hi - lo, n), generator=g, device=dev)
+                    ).clamp_(0.0, float(np.nextafter(np.float32(1), np.float32(0))))
+    return X
+
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mnist")
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--m", type=int, default=60000)
-    ap.add_argument("--n", type=int, default=784)
-    ap.add_argument("--k", type=int, default=30)
+    ap.add_argument("--m", type=int, default=None)
     args = ap.parse_args()
 
     import torch
     import mpiknn
     import mpiknn.ring as ring
-    from mpiknn import synth
 
     dev = torch.device("cuda", 0)
-    m, n, k = args.m, args.n, args.k
-    X, _ = synth.mnist_like(m, n)
-    Xd = torch.from_numpy(X).to(dev)
+    m0, n, k, dt = WORKLOADS[args.workload]
+    m = args.m or m0
+    Xd = corpus(torch, args.workload, m, n, dev)
     res = {}
     for P in [int(p) for p in args.ranks.split(",")]:
         R, blocks = ring.partition(m, P)
-        eng = ring.GpuEngine(torch, 0, n, R, blocks[0][1], k)
+        eng = ring.GpuEngine(torch, 0, n, R, blocks[0][1], k, dtype=dt)
+        sdt = "f32" if Xd.dtype == torch.float32 else "f64"
         eng.pack(Xd[0:blocks[0][1]], layout_col=False)
-        nb = mpiknn.block_bytes(R, n)
+        nb = mpiknn.block_bytes(R, n, dt)
         bufs = []
         for b, (base, rows) in enumerate(blocks):
             t = torch.zeros(nb, dtype=torch.uint8, device=dev)
             mpiknn.block_pack(t.data_ptr(), R, rows, n, Xd[base:base + rows].data_ptr(), n,
-                              mpiknn.ROWMAJOR, eng.stream())
+                              mpiknn.ROWMAJOR, eng.stream(), dtype=dt, src_dtype=sdt)
             bufs.append(t)
             mb = t[eng.meta_off:eng.meta_off + 8 * mpiknn.META_DOUBLES].view(torch.float64)
             eng.meta.copy_(torch.maximum(eng.meta, mb))   # the ring's all_reduce(MAX)
+        h_meta = eng.meta.cpu().numpy()
 
-        # what the ring moves: shadow blocks when the search stages fp16
-        # shadow rows (mpiknn/ring.py), element blocks otherwise
-        eng.begin(0)
-        shadow = P > 1 and eng.ctx.shadow() == 1
-        for b, (base, rows) in enumerate(blocks):
-            eng.step(bufs[b], rows, base)
-        eng.end()
+        # what the ring moves: the search's shadow form when it has one
+        eng.begin(0, h_meta=h_meta)
+        shadow = P > 1 and eng.ctx.shadow() != 0
         sbufs = []
         if shadow:
             for t in bufs:
-                sb = torch.empty(mpiknn.shadow_bytes(R, n), dtype=torch.uint8, device=dev)
-                mpiknn.shadow_pack(sb.data_ptr(), t.data_ptr(), R, n, "f64", eng.stream())
+                sb = torch.empty(eng.ctx.shadow_bytes(R), dtype=torch.uint8, device=dev)
+                eng.ctx.shadow_pack(sb.data_ptr(), t.data_ptr(), R, eng.stream())
                 sbufs.append(sb)
+        for b, (base, rows) in enumerate(blocks):
+            eng.step(bufs[b], rows, base)
+        eng.end()
 
         def one():
-            eng.begin(0)
+            eng.begin(0, h_meta=h_meta)
             for b, (base, rows) in enumerate(blocks):
                 if shadow:
                     eng.step_shadow(sbufs[b], rows, base)
@@ -81,23 +117,27 @@ def main():
         torch.cuda.synchronize()
         eng.ctx.profile(1)
         t0 = time.perf_counter()
+        unres = 0
         for _ in range(args.steps):
-            one()
+            unres += one()
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / args.steps
+        dt_s = (time.perf_counter() - t0) / args.steps
         dist_ms, merge_ms, launches = eng.ctx.profile(0)
         flops = 2.0 * blocks[0][1] * m * n * args.steps
-        res[P] = {"rank_ms": dt * 1e3, "dist_busy_ms_per_pass": dist_ms / args.steps,
+        res[P] = {"rank_ms": dt_s * 1e3, "dist_busy_ms_per_pass": dist_ms / args.steps,
                   "dist_tflops": flops / (dist_ms * 1e-3) / 1e12 if dist_ms > 0 else None,
                   "exposed_merge_ms_per_pass": merge_ms / args.steps,
-                  "splits": eng.ctx.info()[1], "shadow_ring": shadow}
+                  "splits": eng.ctx.info()[1], "shadow_ring": shadow,
+                  "contraction_bits": eng.ctx.contraction_bits(), "unresolved": unres}
+        print(json.dumps({"P": P, **res[P]}), file=sys.stderr, flush=True)
         del bufs, sbufs, eng
         torch.cuda.empty_cache()
-    t1 = res[min(res)]["rank_ms"]
+    t1 = res[min(res)]["rank_ms"] * min(res)
     for P, r in res.items():
         r["projected_qps"] = m / (r["rank_ms"] * 1e-3)
         r["compute_efficiency"] = t1 / (P * r["rank_ms"])
-    print(json.dumps(res, indent=1))
+    print(json.dumps({"workload": args.workload, "m": m, "n": n, "k": k, "dtype": dt,
+                      "ranks": res}, indent=1))
 
 
 if __name__ == "__main__":
