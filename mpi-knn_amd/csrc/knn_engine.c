@@ -688,7 +688,7 @@ static int launch_merge_sets(knn_ctx_t *c, int set, int nsets, int nsplit_total,
     RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
                           nsplit_total, c->lpq, c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x,
                           c->st_i, c->st_T, c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n,
-                          c->meta, c->ms));
+                          c->meta, c->qthr, c->ms));
     c->merged = 1;
     for (int x = 0; x < nsets; x++) HIPCHK(hipEventRecord(c->ev_m[(set + x) % KNN_PSETS], c->ms));
     return KNN_OK;

@@ -117,7 +117,7 @@ int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *
                      int first_step,
                      double *st_d, double *st_x, int *st_i, double *st_T, const void *qblk,
                      size_t q_rows_pad, const void *cblk, size_t c_base, int nc, int n,
-                     const double *meta, void *stream);
+                     const double *meta, double *qthr, void *stream);
 int knn_launch_finalize(int dtype, int kp, const double *st_d, const double *st_x, const int *st_i,
                         const double *st_T, const void *qblk, size_t q_rows_pad,
                         int nq, int n, int k, const double *meta,

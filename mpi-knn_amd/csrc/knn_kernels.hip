@@ -830,7 +830,7 @@ __global__ __launch_bounds__(256) void k_merge(
     double *__restrict__ st_d, double *__restrict__ st_x, int *__restrict__ st_i,
     double *__restrict__ st_T, const TE *__restrict__ qblk, size_t qnorm_off,
     const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
-    const double *__restrict__ meta, int k)
+    const double *__restrict__ meta, int k, unsigned long long *__restrict__ qthr)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + wave;
@@ -902,6 +902,31 @@ __global__ __launch_bounds__(256) void k_merge(
             hd = (pos < len) ? src_d[pos] : KNN_INF;
             hi = (pos < len) ? src_i[pos] : 0x7fffffff;
             if (hd == KNN_INF) hi = 0x7fffffff;
+        }
+    }
+
+    // INT mode (exact d^2): the new state's (k+1)-th nonzero entry bounds
+    // the query's (k+1)-th candidate over all rows (k+1 distinct rows lie at
+    // or below it) -- the distance kernels' qthr contract.  Published, it
+    // lets every later ring step filter with the running answer instead of
+    // the bound one split's lane lists reach (about the 32nd of that split's
+    // rows).  fp32 blocks: rounded up to an fp32 value, as the kernels read
+    // it back in fp32.
+    if (qthr != nullptr && mode == KNN_MODE_INT) {
+        int z = 0;
+#pragma unroll
+        for (int x = 0; x < NS; x++) z += __popcll(__ballot(lane + 64 * x < KP && sd[x] == 0.0));
+        const int rk = k + z;
+        if (rk < KP) {
+            double u = KNN_INF;
+#pragma unroll
+            for (int x = 0; x < NS; x++) {
+                const double v = __shfl(sd[x], rk & 63);
+                if ((rk >> 6) == x) u = v;
+            }
+            if constexpr (sizeof(TE) == 4) u = (double)__double2float_ru(u);
+            if (lane == 0 && u < KNN_INF)
+                atomicMin(qthr + q, (unsigned long long)__double_as_longlong(u));
         }
     }
 
@@ -1610,7 +1635,7 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
                                 int first_step, double *st_d, double *st_x, int *st_i,
                                 double *st_T, const void *qblk, size_t q_rows_pad,
                                 const void *cblk, size_t c_base, int nc, int n,
-                                const double *meta, void *stream)
+                                const double *meta, double *qthr, void *stream)
 {
     if (lpq < 1 || kl < 1 || lpq * nsplit + 1 > 64 || k <= 0 || k > kp) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
@@ -1620,7 +1645,8 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
 #define CALL(T, KL, KP)                                                                         \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP>), grid, dim3(256), 0, s, part_d, part_i,    \
                        part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x, st_i, st_T,   \
-                       (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n, np, meta, k);    \
+                       (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n, np, meta, k,       \
+                       (unsigned long long *)qthr);                                              \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL

@@ -1,0 +1,80 @@
+# One GPU session: the steps named on the command line, in order, each under
+# its own time limit; the session stops at the first step that fails.
+#
+#   gpurun -- bash tools/gpu.sh STEP [STEP ...]
+#
+# Steps (outputs under gpurun_out/<tag>/):
+#   tests[:EXPR]          pytest -m gpu (optionally -k EXPR); then smoke()
+#   bench:WL[:STEPS]      bench.py --workload WL (CPU leg included)
+#   trace:WL              rocprofv3 --kernel-trace --stats of a bench run
+#   pmc:WL:REP            FETCH_SIZE, WRITE_SIZE, MFMA-busy passes (REP
+#                         repetitions of each, one counter group per run)
+#   emu:WL[:RANKS]        tools/ring_emulate.py (per-rank ring work)
+#   emutrace:WL:RANKS     the same under --kernel-trace
+#   kb8:ARGS              tools/probe/kbench8.py ARGS (commas kept, '+' = space)
+set -o pipefail
+mkdir -p gpurun_out
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+fail() { echo "step $1 rc=$2"; exit "$2"; }
+
+run_step() {
+  local spec=$1 kind a b
+  kind=${spec%%:*}
+  a=$(echo "$spec" | cut -s -d: -f2)
+  b=$(echo "$spec" | cut -s -d: -f3)
+  case $kind in
+  tests)
+    local K=()
+    [ -n "$a" ] && K=(-k "$a")
+    timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu --timeout 150 --timeout-method thread "${K[@]}" \
+      > gpurun_out/pytest.log 2>&1 || { rc=$?; tail -30 gpurun_out/pytest.log; fail "$spec" $rc; }
+    tail -2 gpurun_out/pytest.log
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+      || { rc=$?; tail -20 gpurun_out/smoke.log; fail smoke $rc; }
+    echo "smoke ok" ;;
+  bench)
+    local st=${b:-5}
+    timeout -k 10 500 python -u bench.py --workload "$a" --steps "$st" --warmup 2 > "gpurun_out/bench_$a.log" 2>&1 \
+      || { rc=$?; tail -20 "gpurun_out/bench_$a.log"; fail "$spec" $rc; }
+    grep '^{' "gpurun_out/bench_$a.log" | tail -1 ;;
+  trace)
+    (cd /tmp && export TMPDIR=/tmp && cd "$ROOT" &&
+     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/trace_$a" -o run -- \
+       python3 bench.py --workload "$a" --no-cpu-baseline --check 0 --steps 5 --warmup 2 \
+       > "gpurun_out/trace_$a.log" 2>&1) || fail "$spec" $? ;;
+  pmc)
+    local rep=${b:-3} i g
+    for i in $(seq 1 "$rep"); do
+      for g in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_WAVE_CYCLES"; do
+        local tag
+        tag=$(echo "$g" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+        (cd /tmp && export TMPDIR=/tmp && cd "$ROOT" &&
+         timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/pmc_$a/${tag}_$i" -o run \
+           --pmc $g -- python3 bench.py --workload "$a" --no-cpu-baseline --check 0 --steps 1 --warmup 0 \
+           > "gpurun_out/pmc_$a/${tag}_$i.log" 2>&1) || fail "$spec:$tag:$i" $?
+      done
+    done ;;
+  emu)
+    timeout -k 10 400 python -u tools/ring_emulate.py --workload "$a" --ranks "${b:-1,2,4,8}" --steps 5 \
+      > "gpurun_out/emu_$a.log" 2>&1 || { rc=$?; tail -20 "gpurun_out/emu_$a.log"; fail "$spec" $rc; }
+    grep '"P"' "gpurun_out/emu_$a.log" ;;
+  emutrace)
+    (cd /tmp && export TMPDIR=/tmp && cd "$ROOT" &&
+     timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/emutrace_$a" -o run -- \
+       python3 tools/ring_emulate.py --workload "$a" --ranks "${b:-8}" --steps 3 \
+       > "gpurun_out/emutrace_$a.log" 2>&1) || fail "$spec" $? ;;
+  kb8)
+    local args=${spec#kb8:}
+    timeout -k 10 300 python -u tools/probe/kbench8.py ${args//+/ } >> gpurun_out/kb8.log 2>&1 \
+      || { rc=$?; tail -20 gpurun_out/kb8.log; fail "$spec" $rc; }
+    grep '^{' gpurun_out/kb8.log | tail -40 ;;
+  *) echo "unknown step $spec"; exit 2 ;;
+  esac
+  return 0
+}
+
+for s in "$@"; do
+  [ "${s%%:*}" = pmc ] && mkdir -p "gpurun_out/pmc_$(echo "$s" | cut -d: -f2)"
+  run_step "$s" || exit $?
+  echo "step $s ok"
+done

@@ -43,7 +43,7 @@ extern "C" void kbench8_reset()
 // returns the average kernel ms over iters launches (after one warm-up)
 extern "C" float kbench8(int abl, const void *qsh, size_t q_rows_pad, int nq, const void *csh,
                          size_t c_rows_pad, int nc, int n, int k, int nsplit, double *part_d,
-                         int *part_i, double *part_T, int nq_pad, double *qthr, int iters)
+                         int *part_i, double *part_T, int nq_pad, double *qthr, int iters, int reset)
 {
     const int rs = (int)knn_s8_rs((size_t)n), nks = rs / 32, nch = (nks + 3) / 4;
     const int nqb = (nq + 127) / 128, ntiles = (nc + 127) / 128;
@@ -56,7 +56,7 @@ extern "C" float kbench8(int abl, const void *qsh, size_t q_rows_pad, int nq, co
     hipEventCreate(&e1);
     float total = 0.f;
     for (int it = 0; it <= iters; it++) {
-        hipLaunchKernelGGL(kb8_fill_inf, dim3((nq_pad + 255) / 256), dim3(256), 0, 0, qthr, nq_pad);
+        if (reset || it == 0) hipLaunchKernelGGL(kb8_fill_inf, dim3((nq_pad + 255) / 256), dim3(256), 0, 0, qthr, nq_pad);
         hipEventRecord(e0, 0);
 #define KB(A) case A: kb8_launch<A>(grid, 0, qsh, q_rows_pad, nq, csh, c_rows_pad, nc, rs, nks, ntiles, nsplit, nqb, part_d, part_i, part_T, nq_pad, qthr, uj, nch); break;
         switch (abl) {

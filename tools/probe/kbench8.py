@@ -24,8 +24,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="mnist")
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--splits", type=int, default=0)
+    ap.add_argument("--splits", default="", help="comma list")
     ap.add_argument("--abl", default="0,1,2,4,8,16")
+    ap.add_argument("--keep-qthr", action="store_true",
+                    help="timed launches start from the previous launch's bounds (converged)")
+    ap.add_argument("--m", type=int, default=0, help="use the first M rows (queries = corpus)")
     a = ap.parse_args()
     so = os.path.join(HERE, "libkbench8.so")
     if not os.path.exists(so):
@@ -40,7 +43,8 @@ def main():
     else:
         X = synth.sift_like(1000000, 128)
         k, dt, splits = 32, "f32", 3
-    splits = a.splits or splits
+    if a.m:
+        X = np.ascontiguousarray(X[:a.m])
     m, n = X.shape
     eng = ring.GpuEngine(torch, 0, n, m, m, k, dtype=dt)
     eng.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
@@ -52,21 +56,24 @@ def main():
     nq_pad = (m + 127) // 128 * 128
     rp = nq_pad
     kl = 17   # KNN_I8_KL, 4 lists a query
-    pd = torch.empty(splits * nq_pad * 4 * kl, dtype=torch.float64, device="cuda:0")
-    pi = torch.empty(splits * nq_pad * 4 * kl, dtype=torch.int32, device="cuda:0")
-    pT = torch.empty(splits * nq_pad, dtype=torch.float64, device="cuda:0")
+    smax = max(int(x) for x in (a.splits or str(splits)).split(","))
+    pd = torch.empty(smax * nq_pad * 4 * kl, dtype=torch.float64, device="cuda:0")
+    pi = torch.empty(smax * nq_pad * 4 * kl, dtype=torch.int32, device="cuda:0")
+    pT = torch.empty(smax * nq_pad, dtype=torch.float64, device="cuda:0")
     qthr = torch.empty(nq_pad, dtype=torch.float64, device="cuda:0")
     L = ctypes.CDLL(so)
     p, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
-    L.kbench8.argtypes = [i, p, sz, i, p, sz, i, i, i, i, p, p, p, i, p, i]
+    L.kbench8.argtypes = [i, p, sz, i, p, sz, i, i, i, i, p, p, p, i, p, i, i]
     L.kbench8.restype = ctypes.c_float
     flop = 2.0 * m * m * n
     cnt = (ctypes.c_ulonglong * 4)()
-    for abl in [int(x) for x in a.abl.split(",")]:
+    for abl, splits in [(int(x), int(s)) for x in a.abl.split(",")
+                        for s in (str(a.splits) if a.splits else str(splits)).split(",")]:
         L.kbench8_reset()
         ms = L.kbench8(abl, sb.data_ptr(), rp, m, sb.data_ptr(), rp, m, n, k, splits,
-                       pd.data_ptr(), pi.data_ptr(), pT.data_ptr(), nq_pad, qthr.data_ptr(), a.iters)
-        rec = {"workload": a.workload, "abl": abl, "splits": splits, "ms": ms,
+                       pd.data_ptr(), pi.data_ptr(), pT.data_ptr(), nq_pad, qthr.data_ptr(), a.iters,
+                       0 if a.keep_qthr else 1)
+        rec = {"workload": a.workload, "m": m, "keep_qthr": a.keep_qthr, "abl": abl, "splits": splits, "ms": ms,
                "tops": flop / (ms * 1e-3) / 1e12 if ms > 0 else None}
         if abl & 32:
             L.kbench8_counters(cnt)
