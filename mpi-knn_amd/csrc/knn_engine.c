@@ -67,7 +67,7 @@ struct knn_ctx {
     /* overlapped step schedule (knn_ctx_step): distance kernels alternate
      * over two streams, merges run in order on a third */
     hipStream_t ds[2], ms;
-    hipEvent_t ev_in, ev_d[2], ev_m[KNN_PSETS];
+    hipEvent_t ev_in, ev_d[2], ev_m[KNN_PSETS], ev_ds[KNN_PSETS];
     int nstep;
     /* per-query filter bound shared by all splits and ring steps */
     double *qthr;
@@ -225,8 +225,10 @@ int knn_block_pack(void *d_block, size_t cap, size_t rows, size_t n, const doubl
 
 static void ctx_free_buffers(knn_ctx_t *c)
 {
-    for (int b = 0; b < KNN_PSETS; b++)
+    for (int b = 0; b < KNN_PSETS; b++) {
         if (c->ev_m[b]) hipEventDestroy(c->ev_m[b]);
+        if (c->ev_ds[b]) hipEventDestroy(c->ev_ds[b]);
+    }
     for (int b = 0; b < KNN_PSETS / 2; b++) {
         hipFree(c->pp_d[b]);
         hipFree(c->pp_i[b]);
@@ -373,8 +375,10 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
         ok &= hipStreamCreateWithFlags(&c->ds[b], hipStreamNonBlocking) == hipSuccess;
         ok &= hipEventCreateWithFlags(&c->ev_d[b], hipEventDisableTiming) == hipSuccess;
     }
-    for (int b = 0; b < KNN_PSETS; b++)
+    for (int b = 0; b < KNN_PSETS; b++) {
         ok &= hipEventCreateWithFlags(&c->ev_m[b], hipEventDisableTiming) == hipSuccess;
+        ok &= hipEventCreateWithFlags(&c->ev_ds[b], hipEventDisableTiming) == hipSuccess;
+    }
     /* merges are short and gate the next steps: highest priority */
     int prio_lo = 0, prio_hi = 0;
     hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
@@ -711,7 +715,10 @@ static int merge_pending(knn_ctx_t *c)
  *            arrived, begin() is done) and ev_m[p] (merge s-4 has read the
  *            partial set), then k_dist_topk(s)              -> ev_d[s%2]
  *   ms:      wait ev_d[s%2] and ev_in, then k_merge(s)      -> ev_m[p]
- *   caller:  wait ev_m[(s-2)%4] (step s-2 has finished reading its block)
+ *   caller:  wait ev_m[(s-2)%4] (step s-2 has finished reading its block);
+ *            exact-integer contractions (int8 / fp16: k_merge never reads
+ *            block rows) wait ev_ds[(s-2)%4], k_dist_topk(s-2) alone, so
+ *            no merge sits on the chain that gates the next blocks
  * so k_dist_topk(s) starts while k_dist_topk(s-1) drains its last
  * workgroups -- a ring step no longer pays its launch tail -- and the
  * merges (which co-reside with the distance workgroups and so stretch
@@ -804,6 +811,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
                                   ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
     HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
+    HIPCHK(hipEventRecord(c->ev_ds[set], ds));
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_in, 0));
     if (pairing) {
@@ -827,8 +835,10 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
         if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
     }
     /* step s - 2 is merged by now (a pending step is always s itself) */
-    if (c->nstep >= KNN_STEP_LAG)
-        HIPCHK(hipStreamWaitEvent(cs, c->ev_m[(c->nstep - KNN_STEP_LAG) % KNN_PSETS], 0));
+    if (c->nstep >= KNN_STEP_LAG) {
+        const int ps = (c->nstep - KNN_STEP_LAG) % KNN_PSETS;
+        HIPCHK(hipStreamWaitEvent(cs, (c->i8 || c->h16) ? c->ev_ds[ps] : c->ev_m[ps], 0));
+    }
     c->first_step = 0;
     c->nstep++;
     return KNN_OK;

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--keep-qthr", action="store_true",
                     help="timed launches start from the previous launch's bounds (converged)")
     ap.add_argument("--m", type=int, default=0, help="use the first M rows (queries = corpus)")
+    ap.add_argument("--ideal-qthr", action="store_true",
+                    help="bounds preset to each query's (k+1)-th d^2 over the FULL set (a late ring step)")
     a = ap.parse_args()
     so = os.path.join(HERE, "libkbench8.so")
     if not os.path.exists(so):
@@ -43,6 +45,7 @@ def main():
     else:
         X = synth.sift_like(1000000, 128)
         k, dt, splits = 32, "f32", 3
+    Xfull = X
     if a.m:
         X = np.ascontiguousarray(X[:a.m])
     m, n = X.shape
@@ -61,6 +64,19 @@ def main():
     pi = torch.empty(smax * nq_pad * 4 * kl, dtype=torch.int32, device="cuda:0")
     pT = torch.empty(smax * nq_pad, dtype=torch.float64, device="cuda:0")
     qthr = torch.empty(nq_pad, dtype=torch.float64, device="cuda:0")
+    if a.ideal_qthr:
+        # (k+1)-th nonzero d^2 of each query over all rows (exact: integer
+        # data, fp64 sums far below 2^53)
+        F = torch.from_numpy(np.ascontiguousarray(Xfull)).to("cuda:0").double()
+        Q = F[:m]
+        nrm = (F * F).sum(1)
+        b = torch.full((nq_pad,), float("inf"), dtype=torch.float64, device="cuda:0")
+        for lo in range(0, m, 1024):
+            hi = min(m, lo + 1024)
+            d2 = nrm[lo:hi, None] + nrm[None, :] - 2.0 * Q[lo:hi] @ F.t()
+            d2[d2 <= 0] = float("inf")
+            b[lo:hi] = torch.topk(d2, k + 1, dim=1, largest=False).values[:, k]
+        qthr.copy_(b)
     L = ctypes.CDLL(so)
     p, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     L.kbench8.argtypes = [i, p, sz, i, p, sz, i, i, i, i, p, p, p, i, p, i, i]
@@ -72,8 +88,8 @@ def main():
         L.kbench8_reset()
         ms = L.kbench8(abl, sb.data_ptr(), rp, m, sb.data_ptr(), rp, m, n, k, splits,
                        pd.data_ptr(), pi.data_ptr(), pT.data_ptr(), nq_pad, qthr.data_ptr(), a.iters,
-                       0 if a.keep_qthr else 1)
-        rec = {"workload": a.workload, "m": m, "keep_qthr": a.keep_qthr, "abl": abl, "splits": splits, "ms": ms,
+                       2 if a.ideal_qthr else (0 if a.keep_qthr else 1))
+        rec = {"workload": a.workload, "m": m, "keep_qthr": a.keep_qthr, "ideal": a.ideal_qthr, "abl": abl, "splits": splits, "ms": ms,
                "tops": flop / (ms * 1e-3) / 1e12 if ms > 0 else None}
         if abl & 32:
             L.kbench8_counters(cnt)
