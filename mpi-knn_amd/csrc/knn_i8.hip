@@ -192,13 +192,11 @@ __global__ __launch_bounds__(256) void k_shadow8(signed char *__restrict__ dst, 
 // busiest lane per tile.  d^2 is exact, so "S != 0" (serial:86) is d^2 > 0,
 // applied at the merge.
 //
-// ABL: ablations for the tuning harness tools/probe/kbench8 only (libknn
-// instantiates ABL = 0): 1 no epilogue, 2 keys + lane minimum only, 4 no
-// staging DMA, 8 no chunk wait/barrier, 16 no MFMA, 32 count wave-tiles with
-// survivors and insertion rounds into i8_dbg.
+// Ablations of this kernel (no epilogue, keys only, no DMA, no barrier, no
+// MFMA, survivor counters) were measured with the tuning
+// harness at commit 8ea8e2a; the product source carries no hooks.
 // ---------------------------------------------------------------------------
-__device__ unsigned long long i8_dbg[4];   // tuning harness only (ABL 32)
-template <int KL, int NKS, int W, int WPS, int NST, int NB, int ABL = 0>
+template <int KL, int NKS, int W, int WPS, int NST, int NB>
 __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     const signed char *__restrict__ qsh, size_t q_rows_pad, size_t q_base, int nq,
     const signed char *__restrict__ csh, size_t c_rows_pad, size_t c_base, int nc, int rs,
@@ -285,7 +283,6 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
     int s_t = t_lo, s_c = 0, s_x = 0;
     auto stage = [&]() {
-        if constexpr ((ABL & 4) != 0) { s_x++; return; }
         const signed char *base = csh + (size_t)s_t * 128 * rs + 128 * s_c;
         const unsigned dst = lds0 + (unsigned)(s_x % NST) * 16384u + (unsigned)wave_s * (16384u / W);
         if constexpr (PW == 4) bglds16x4(knn_rsrc(base), voff[0], voff[1], voff[2], voff[3], dst);
@@ -306,7 +303,6 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // the next chunk's own pieces landed: the NST - 3 chunks staged after it
     // may stay in flight
     auto wait_next = [&]() {
-        if constexpr ((ABL & 8) != 0) return;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (NST - 3)) : "memory");
     };
     // A fragments (MB m-blocks) of K-step ks of staged chunk xx
@@ -364,10 +360,6 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
 
     // ---- epilogue of tile t --------------------------------------------------
     auto epilogue = [&](int t, knn_v16i (&A)[MB]) {
-        if constexpr ((ABL & 1) != 0) {
-            L[0] = min(L[0], A[0][0] ^ A[MB - 1][3]);
-            return;
-        }
         const LDS_AS knn_v4i *cn =
             (const LDS_AS knn_v4i *)((LDS_AS char *)smem + NORM0 + (t % NST) * 512) + 4 * h + 8 * MB * rh;
         const int lim = L[KL - 1] < thr ? L[KL - 1] : thr;
@@ -390,13 +382,6 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 32 * qg;
         const bool masked = (row0 + 32 * MB > nc) || (gw0 < gt0 + 32 * MB && gt0 < gw0 + 32);
         if (!masked && __ballot(lmn <= limq) == 0ull) return;   // common late in the scan
-        if constexpr ((ABL & 2) != 0) {
-            L[0] = min(L[0], lmn);
-            return;
-        }
-        if constexpr ((ABL & 32) != 0) {
-            if (lane == 0) atomicAdd(&i8_dbg[0], 1ull);
-        }
         const int idb = (int)(c_base + row0) + 4 * h;
         // survivors of G m-blocks at a time (W = 8: both, one 32-bit mask):
         // one wave round per survivor of the busiest lane; each lane takes its
@@ -439,9 +424,6 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                     cnt++;
                 }
                 pend &= pend - 1;
-                if constexpr ((ABL & 32) != 0) {
-                    if (lane == 0) atomicAdd(&i8_dbg[1], 1ull);
-                }
                 if (__ballot(cnt == NB) != 0ull) merge();
             }
         }
@@ -473,16 +455,14 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                             rdA(x, ks + 1, anxt);
                         } else if (x + 1 < total) {
                             wait_next();
-                            if constexpr ((ABL & 8) == 0) __builtin_amdgcn_s_barrier();   // B(x + 1)
+                            __builtin_amdgcn_s_barrier();   // B(x + 1)
                             rdA(x + 1, 0, anxt);
                             stage();
                         }
-                        if constexpr ((ABL & 16) == 0) {
 #pragma unroll
-                            for (int bb = 0; bb < MB; bb++)
-                                acc[bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(acur[bb], qf[4 * c + ks],
-                                                                                acc[bb], 0, 0, 0);
-                        }
+                        for (int bb = 0; bb < MB; bb++)
+                            acc[bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(acur[bb], qf[4 * c + ks],
+                                                                            acc[bb], 0, 0, 0);
 #pragma unroll
                         for (int bb = 0; bb < MB; bb++) acur[bb] = anxt[bb];
                     }

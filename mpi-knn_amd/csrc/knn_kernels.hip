@@ -307,18 +307,12 @@ __global__ __launch_bounds__(256) void k_norms(T *__restrict__ blk, size_t rows,
 //   4*32K:            corpus norms ring [tile&7][g][32]
 // ---------------------------------------------------------------------------
 #define KNN_NST 4
-__device__ unsigned long long knn_dbg_rounds[256];   // tuning harness only (EPI 3)
-
-// EPI != 1 / ABL != 0 exist only for the tuning harness (tools/probe/kbench):
-// EPI 0 skips the top-k insertion, EPI 3 counts insertion rounds per tile
-// position into knn_dbg_rounds.  ABL bits: 0 no staging loads, 1 no chunk
-// barrier, 4 s_setprio 1 on waves 4..7, 5 an m-tile's two k-steps 4 MFMAs
-// apart, 6 / 7 stage every workgroup's queries from block 0 / the corpus
-// from the split's first tile (L2-resident; wrong results), 11 each
-// segment's load before its first MFMA pair, 13 waves 0..3 stage for all
-// eight.  libknn instantiates <.., 1, 0> (element rows) and <.., 1, 8192, 2>
-// (fp16 shadow rows, where bit 13 measured 2% faster).
-template <typename T, int KL, int KS, int EPI = 1, int ABL = 0, int H16 = 0>
+// STG = 1: waves 0..3 stage the chunk pieces of their SIMD partners w + 4 too
+// (fp16 shadow rows of fp32 blocks: sift 607 vs 691 ms); STG = 0: every wave
+// stages its own.  Round-1 ablations of this kernel (no staging, no barrier,
+// no insertion, setprio, MFMA orders: DESIGN.md sec.4) were measured with the
+// tuning harness at commit 1e35c3d; the product source carries no hooks.
+template <typename T, int KL, int KS, int STG = 0, int H16 = 0>
 __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const T *__restrict__ qblk, const T *__restrict__ qnorm, size_t q_base, int nq,
     const T *__restrict__ cblk, const T *__restrict__ cnorm, size_t c_base, int nc,
@@ -378,9 +372,6 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // keys, tightest filter); GEMM mode the whole state (slack for the
     // certificate's error margin)
     const int ujm = (mode == KNN_MODE_INT) ? (uj & 255) : (uj >> 8);
-    if constexpr ((ABL & 16) != 0) {
-        if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
-    }
 
     T L[KL];
     int I[KL];
@@ -441,19 +432,19 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // Every wave stages its own m-tile and its own 16 queries.  All staging
     // addresses are scalar (wave_s, not the VGPR wave index): deriving the
     // LDS destination per load from a VGPR (v_readfirstlane into M0) cost
-    // 2.9 ms.  ABL bit 13 moves all staging to waves 0..3 (they load for
-    // their SIMD partner w+4 too): 0.6 ms slower once addressing is scalar.
+    // 2.9 ms.  STG = 1 moves all staging to waves 0..3 (they load for
+    // their SIMD partner w+4 too): 0.6 ms slower on fp64 element rows once
+    // addressing is scalar.
     const int wave_s = __builtin_amdgcn_readfirstlane(wave);
-    constexpr bool SELF = (ABL & 8192) == 0;
+    constexpr bool SELF = STG == 0;
     const bool loader = SELF || wave_s < 4;
     auto glds1 = [&](int i) {
-        if constexpr ((ABL & 1) != 0) return;
         if (!loader) return;
         const unsigned r8 = 8u * RS * (unsigned)n_pad;             // 8 rows, bytes
         const size_t fo = (size_t)128 * s_fc;                      // chunk offset, bytes
         const char *cb = (const char *)cblk +
-                         (size_t)((ABL & 128) ? t_lo : s_t) * KNN_TC * n_pad * RS + fo;
-        const char *qb0 = (const char *)qblk + (size_t)((ABL & 64) ? 0 : qrow0) * n_pad * RS + fo;
+                         (size_t)s_t * KNN_TC * n_pad * RS + fo;
+        const char *qb0 = (const char *)qblk + (size_t)qrow0 * n_pad * RS + fo;
 #pragma unroll
         for (int hw = 0; hw < (SELF ? 1 : 2); hw++) {
             const int ww = SELF ? wave_s : (wave_s & 3) + 4 * hw;
@@ -477,7 +468,6 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     };
     // norm slice of tile t (clamped to the split) into ring slot `slot`
     auto gnorm = [&](int t, int slot) {
-        if constexpr ((ABL & 1) != 0) return;
         if (!loader) return;
         const int ts = t < t_hi ? t : t_hi - 1;
         const unsigned ndst = (unsigned)(uintptr_t)lds + NST * 32768u + (unsigned)(slot & 7) * 1024u +
@@ -531,11 +521,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
         // zeros (INT-mode exact duplicates) and masked tiles only send the
         // wave down the slow path, where d^2 > 0 and the row mask are
         // applied (masking here made hipcc copy all 32 d^2 at the join)
-        bool any = masked || __ballot(lanemin <= lim) != 0ull;   // rare late in the scan
-        if constexpr (EPI == 0) {
-            L[0] = fmin(L[0], lanemin);
-            any = false;
-        }
+        const bool any = masked || __ballot(lanemin <= lim) != 0ull;   // rare late in the scan
         if (any) {
             // INT mode: d^2 is exact and >= 0, so "S != 0" (serial:86) is d^2 > 0
             const T zfloor = (mode == KNN_MODE_INT) ? (T)0 : (T)-KNN_INF;
@@ -577,9 +563,6 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 const int ii = (int)(c_base + row0 + 16 * (b >> 2) + rowmap(g, b & 3));
                 pend_all &= pend_all - 1;
                 list_insert<KL>(L, I, dd, ii);
-                if constexpr (EPI == 3) {
-                    if (threadIdx.x == 0) atomicAdd(&knn_dbg_rounds[(t - t_lo) < 255 ? t - t_lo : 255], 1ull);
-                }
             }
         }
 #pragma unroll
@@ -614,12 +597,12 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // one segment: 8 MFMAs on quarter h with fragments f and query piece b;
     // between them the reads `rdj(j)` of the next segment and one staging
     // load `stage()` (sched_barrier-pinned order)
-    constexpr int SJ = (ABL & 2048) ? 0 : 2;   // m-tile pair after which a segment's load issues
+    constexpr int SJ = 2;   // m-tile pair after which a segment's load issues
     // fp64: an m-tile's two k-steps back to back (measured 1.2% faster than
     // interleaving); fp32: v_mfma_f32_16x16x4 has a 40-cycle dependent
     // latency against a 32-cycle issue, so its 4 k-steps go round-robin
-    // over the 4 m-tiles.  ABL bit 5 swaps the two orders.
-    constexpr bool PAIRS = (ES == 8) == ((ABL & 32) == 0);
+    // over the 4 m-tiles.
+    constexpr bool PAIRS = ES == 8;
     auto segment = [&](const frag_t (&f)[4], const frag_t &b, int h, auto &&rdj, auto &&stage) {
         if constexpr (PAIRS) {
 #pragma unroll
@@ -770,7 +753,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                 // S2: (p1, mt0-3) on f0 || read (p1, mt4-7) into f1
                 segment(f0, b1, 0, [&](int j) { rd(cs, 1, 1, f1, j); }, [&]() { glds1(3); });
                 advance();
-                if constexpr ((ABL & 2) == 0) {
+                {
                     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this stage's reads done
                     // chunk c+1 landed: chunks c+2, c+3 may stay in flight
                     if constexpr (SELF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -1570,20 +1553,20 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     if ((flags & KNN_DIST_SHADOW) && (flags & KNN_DIST_H16)) {
         if (!qsh || !csh) return KNN_ERR_INVALID;
         const int nps = (int)knn_round_up((size_t)n, 64);   // shadow row length (halves)
-        // shadow rows: waves 0..3 may stage for their SIMD partners too (ABL
-        // bit 13; partial lists byte-identical, tools/probe/kbench16)
-        // Every wave stages its own rows (ABL 0) for fp64 blocks (mnist 10.0
+        // shadow rows: waves 0..3 may stage for their SIMD partners too (STG
+        // 1; partial lists byte-identical)
+        // Every wave stages its own rows (STG 0) for fp64 blocks (mnist 10.0
         // vs 10.1 ms); fp32 (sift) 607 vs 691 ms with waves 0..3 staging.
         // KNN_STAGE_ALL=0/1 overrides.
         static const char *sa_env = getenv("KNN_STAGE_ALL");
         const int stage_all = sa_env ? sa_env[0] == '1' : (int)(sizeof(T) == 8);
         if (stage_all)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 0, 2>), grid, dim3(512), 0, s,
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 2>), grid, dim3(512), 0, s,
                                (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
                                nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
                                (unsigned long long *)qthr, uj, xord);
         else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 8192, 2>), grid, dim3(512), 0, s,
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 2>), grid, dim3(512), 0, s,
                                (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
                                nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
                                (unsigned long long *)qthr, uj, xord);
@@ -1591,7 +1574,7 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     }
     {
         if (flags & KNN_DIST_H16) {   // host-checked: INT mode and max|x| <= 2048 (fp64: 256)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 0, 1>), grid, dim3(512), 0, s,
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 1>), grid, dim3(512), 0, s,
                                qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles, nsplit,
                                nqb, meta, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr,
                                uj, xord);

@@ -147,3 +147,43 @@ def test_wire_round_trip(knn, dtype):
     assert torch.equal(back, e.qb)
     X[0, 0] = 32768.0
     assert not knn.wire_ok(np.array([32768.0, 0, 0, 0, 0, 0, 0, 0]))
+
+
+@pytest.mark.parametrize("P", [2, 8])
+@pytest.mark.parametrize("shape", ["gist", "sift"])
+def test_ring_search_fp32_configs(knn, oracle, P, shape):
+    """configs[4] / configs[3] shapes through the real ring_search at reduced
+    m: gist-like (real-valued fp32, n = 960, k = 100: fp32 GEMM filter +
+    exact re-rank, element blocks on the link) and sift-like (integer fp32,
+    n = 128, k = 32: int8 byte blocks on the link).  Every rank equals the
+    oracle on the fp32-rounded points (the fp32 contract, test_gpu_f32.py)."""
+    import torch
+    import mpiknn.ring as ring
+
+    if shape == "gist":
+        X, k = datasets.gist_like(1200, 960, clusters=32), 100
+    else:
+        X, k = datasets.sift_like(3000, 128, clusters=64, seed=7), 32
+    X32 = np.ascontiguousarray(X, dtype=np.float32)
+    Xr = X32.astype(np.float64)
+    m, n = X32.shape
+    dev = torch.device("cuda", 0)
+    Xd = torch.from_numpy(X32).to(dev)
+    R, blocks = ring.partition(m, P)
+    engines = []
+    for g in range(P):
+        base, rows = blocks[g]
+        e = ring.GpuEngine(torch, 0, n, R, rows, k, dtype="f32")
+        e.pack(Xd[base:base + rows], layout_col=False)
+        engines.append(e)
+    packed = [e.qb.clone() for e in engines]
+    metas = torch.stack([e.meta for e in engines])
+    for g, e in enumerate(engines):
+        base, rows = blocks[g]
+        d = loopback_dist(torch, g, P, packed, metas, packed, e)
+        ring.ring_search(d, torch, e, g, P, m, base)
+        got = e.result()
+        ref = oracle.knn(Xr, k, rows=(base, rows))
+        assert np.array_equal(got["idx"], ref["idx"]), (shape, P, g)
+        assert np.array_equal(got["distance"].view(np.uint64),
+                              ref["distance"].view(np.uint64)), (shape, P, g)

@@ -1,11 +1,11 @@
-"""Drive tools/probe/kbench8 (k_dist_topk_i8 ablations) on real engine data.
+"""Drive tools/probe/kbench8 (k_dist_topk_i8 timings) on real engine data.
 
-  python tools/probe/kbench8.py [--workload mnist|sift] [--iters 5] [--abl 0,1,2,...]
+  python tools/probe/kbench8.py [--workload mnist|sift] [--iters 5]
+         [--variant 0,1] [--splits 4,6] [--m M] [--keep-qthr | --ideal-qthr]
 
-ABL bits (k_dist_topk_i8's tuning argument): 1 no epilogue, 2 epilogue
-keys + lane minimum only (no insertion), 4 no staging DMA (garbage data),
-8 no chunk wait/barrier (racy), 16 no MFMA.  Variant 0 is the product
-kernel.  Prints one JSON line per variant."""
+Variant 0 is the product instantiation; 1 is mnist with an 8-stage staging
+ring and 6-entry survivor buffers.  Prints one JSON line per (variant,
+splits)."""
 import argparse
 import ctypes
 import json
@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--workload", default="mnist")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--splits", default="", help="comma list")
-    ap.add_argument("--abl", default="0,1,2,4,8,16")
+    ap.add_argument("--variant", default="0")
     ap.add_argument("--keep-qthr", action="store_true",
                     help="timed launches start from the previous launch's bounds (converged)")
     ap.add_argument("--m", type=int, default=0, help="use the first M rows (queries = corpus)")
@@ -82,21 +82,14 @@ def main():
     L.kbench8.argtypes = [i, p, sz, i, p, sz, i, i, i, i, p, p, p, i, p, i, i]
     L.kbench8.restype = ctypes.c_float
     flop = 2.0 * m * m * n
-    cnt = (ctypes.c_ulonglong * 4)()
-    for abl, splits in [(int(x), int(s)) for x in a.abl.split(",")
+    for var, splits in [(int(x), int(s)) for x in a.variant.split(",")
                         for s in (str(a.splits) if a.splits else str(splits)).split(",")]:
-        L.kbench8_reset()
-        ms = L.kbench8(abl, sb.data_ptr(), rp, m, sb.data_ptr(), rp, m, n, k, splits,
+        ms = L.kbench8(var, sb.data_ptr(), rp, m, sb.data_ptr(), rp, m, n, k, splits,
                        pd.data_ptr(), pi.data_ptr(), pT.data_ptr(), nq_pad, qthr.data_ptr(), a.iters,
                        2 if a.ideal_qthr else (0 if a.keep_qthr else 1))
-        rec = {"workload": a.workload, "m": m, "keep_qthr": a.keep_qthr, "ideal": a.ideal_qthr, "abl": abl, "splits": splits, "ms": ms,
+        rec = {"workload": a.workload, "m": m, "keep_qthr": a.keep_qthr, "ideal": a.ideal_qthr,
+               "variant": var, "splits": splits, "ms": ms,
                "tops": flop / (ms * 1e-3) / 1e12 if ms > 0 else None}
-        if abl & 32:
-            L.kbench8_counters(cnt)
-            runs = a.iters + 1
-            wave_tiles = (m // 128 + 1) * splits * 8 * ((m // 128 + 1) // splits)
-            rec.update(survivor_wave_tiles=cnt[0] / runs, rounds=cnt[1] / runs,
-                       wave_tiles_approx=wave_tiles)
         print(json.dumps(rec), flush=True)
 
 
