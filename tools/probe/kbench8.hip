@@ -12,8 +12,9 @@ __global__ void kb8_fill_inf(double *p, int n)
     if (i < n) p[i] = __builtin_inf();
 }
 
-// variant 0: the product's k <= 32 instantiations (sift: 4 K-steps, mnist:
-// 25); variant 1: mnist with an 8-stage ring and 6-entry survivor buffers
+// variant v: (NST, NB) = {0: (7, 8) the product, 1: (8, 6), 2: (8, 4),
+// 3: (7, 6), 4: (7, 4), 5: (8, 5)} at the data's K-step bucket (sift 4,
+// mnist 25)
 template <int NKS, int NST, int NB>
 static void kb8_go(dim3 grid, const void *qsh, size_t q_rows_pad, int nq, const void *csh, size_t c_rows_pad,
                    int nc, int rs, int nks, int ntiles, int nsplit, int nqb, double *part_d, int *part_i,
@@ -36,7 +37,7 @@ extern "C" float kbench8(int variant, const void *qsh, size_t q_rows_pad, int nq
     int uj = (k + 2) / 2 - 1, uj4 = (k + 4) / 4 - 1;   // as knn_launch_dist_i8
     if (uj > KNN_I8_KL - 1) uj = KNN_I8_KL - 1;
     uj |= uj4 << 8;
-    if (nks > 28 || (variant == 1 && nks > 25)) return -1.f;
+    if (nks > 25) return -1.f;
     const dim3 grid((unsigned)(nqb * nsplit));
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -2.f;
@@ -45,15 +46,24 @@ extern "C" float kbench8(int variant, const void *qsh, size_t q_rows_pad, int nq
         if (reset == 1 || (reset == 0 && it == 0))
             hipLaunchKernelGGL(kb8_fill_inf, dim3((nq_pad + 255) / 256), dim3(256), 0, 0, qthr, nq_pad);
         (void)hipEventRecord(e0, 0);
-        if (variant == 1)
-            kb8_go<25, 8, 6>(grid, qsh, q_rows_pad, nq, csh, c_rows_pad, nc, rs, nks, ntiles, nsplit, nqb,
-                             part_d, part_i, part_T, nq_pad, qthr, uj);
-        else if (nks <= 4)
-            kb8_go<4, 7, 8>(grid, qsh, q_rows_pad, nq, csh, c_rows_pad, nc, rs, nks, ntiles, nsplit, nqb,
-                            part_d, part_i, part_T, nq_pad, qthr, uj);
-        else
-            kb8_go<25, 7, 8>(grid, qsh, q_rows_pad, nq, csh, c_rows_pad, nc, rs, nks, ntiles, nsplit, nqb,
-                             part_d, part_i, part_T, nq_pad, qthr, uj);
+#define KB8(NKS, NST, NB) kb8_go<NKS, NST, NB>(grid, qsh, q_rows_pad, nq, csh, c_rows_pad, nc, rs, nks, ntiles, \
+                                               nsplit, nqb, part_d, part_i, part_T, nq_pad, qthr, uj)
+#define KB8V(NKS)                               \
+    switch (variant) {                          \
+    case 1: KB8(NKS, 8, 6); break;              \
+    case 2: KB8(NKS, 8, 4); break;              \
+    case 3: KB8(NKS, 7, 6); break;              \
+    case 4: KB8(NKS, 7, 4); break;              \
+    case 5: KB8(NKS, 8, 5); break;              \
+    default: KB8(NKS, 7, 8); break;             \
+    }
+        if (nks <= 4) {
+            KB8V(4)
+        } else {
+            KB8V(25)
+        }
+#undef KB8V
+#undef KB8
         (void)hipEventRecord(e1, 0);
         (void)hipEventSynchronize(e1);
         float ms = 0.f;
