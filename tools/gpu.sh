@@ -9,7 +9,7 @@
 #   trace:WL              rocprofv3 --kernel-trace --stats of a bench run
 #   pmc:WL:REP            FETCH_SIZE, WRITE_SIZE, MFMA-busy passes (REP
 #                         repetitions of each, one counter group per run)
-#   emu:WL[:RANKS]        tools/ring_emulate.py (per-rank ring work)
+#   emu:WL[:RANKS[:STEPS]] tools/ring_emulate.py (per-rank ring work)
 #   emutrace:WL:RANKS     the same under --kernel-trace
 #   kb8:ARGS              tools/probe/kbench8.py ARGS (commas kept, '+' = space)
 set -o pipefail
@@ -55,7 +55,9 @@ run_step() {
       done
     done ;;
   emu)
-    timeout -k 10 400 python -u tools/ring_emulate.py --workload "$a" --ranks "${b:-1,2,4,8}" --steps 5 \
+    local es
+    es=$(echo "$spec" | cut -s -d: -f4)
+    timeout -k 10 400 python -u tools/ring_emulate.py --workload "$a" --ranks "${b:-1,2,4,8}" --steps "${es:-5}" \
       > "gpurun_out/emu_$a.log" 2>&1 || { rc=$?; tail -20 "gpurun_out/emu_$a.log"; fail "$spec" $rc; }
     grep '"P"' "gpurun_out/emu_$a.log" ;;
   emutrace)

@@ -1,82 +1,109 @@
 #!/usr/bin/env python3
-"""Turn a tools/gpu_round.sh run (gpurun_out/round_<wl>/) into the committed
-evidence under profiles/: the rocprofv3 kernel stats, the PMC traffic that
-bench.py reports as roofline.traffic (merged into profiles/pmc_traffic.json
-under bench.py's key), and a short summary.
+"""Turn a `tools/gpu.sh bench:WL trace:WL pmc:WL:REP` session (files under
+gpurun_out/) into the committed evidence under profiles/: the rocprofv3
+kernel stats, the PMC traffic of the dominant kernel that bench.py reports
+as roofline.traffic (median of the REP passes, merged into
+profiles/pmc_traffic.json under bench.py's key) and a short summary.
 
-  python tools/make_profiles.py <tag> <workload>     e.g.  r01 sift
+  python tools/make_profiles.py <tag> <workload>     e.g.  r02 mnist
 
-HBM bytes follow MI355X_MICROARCH.md sec.HBM: FETCH_SIZE and WRITE_SIZE
-are KiB; on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads,
-so it is doubled.  Counters were collected one group per run with
---kernel-trace only.
+HBM bytes follow MI355X_MICROARCH.md sec.HBM: FETCH_SIZE and WRITE_SIZE are
+KiB; on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads, so
+it is doubled.  Each counter group ran in its own process with
+--kernel-trace only (one bench step, one launch of the distance kernel).
 """
 import csv
 import glob
 import json
 import os
 import shutil
+import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TAG = sys.argv[1] if len(sys.argv) > 1 else "r01"
+TAG = sys.argv[1] if len(sys.argv) > 1 else "r02"
 WL = sys.argv[2] if len(sys.argv) > 2 else "mnist"
-SRC = os.path.join(ROOT, "gpurun_out", "round_" + WL)
+OUT = os.path.join(ROOT, "gpurun_out")
 DST = os.path.join(ROOT, "profiles")
 
 
-def counters(name):
-    fs = glob.glob(os.path.join(SRC, name, "**", "*counter_collection.csv"), recursive=True)
-    out = {}
+def per_launch(pass_dir):
+    """{kernel: {counter: value per dispatch}} of one PMC pass."""
+    fs = glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True)
+    tot, disp = {}, {}
     for f in fs:
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-            out.setdefault(k, {}).setdefault(r["Counter_Name"], 0.0)
-            out[k][r["Counter_Name"]] += float(r["Counter_Value"])
-    return out
+            tot.setdefault(k, {}).setdefault(r["Counter_Name"], 0.0)
+            tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp.setdefault(k, set()).add(r["Dispatch_Id"])
+    return {k: {c: v / len(disp[k]) for c, v in cs.items()} for k, cs in tot.items()}
+
+
+def dominant(d):
+    ks = [k for k in d if k.startswith("k_dist_topk")]
+    return ks[0] if ks else None
 
 
 def main():
     os.makedirs(DST, exist_ok=True)
-    stats = glob.glob(os.path.join(SRC, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    stats = glob.glob(os.path.join(OUT, "trace_" + WL, "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(DST, "%s_%s_kernel_stats.csv" % (TAG, WL)))
-    fetch, write, mfma = counters("fetch"), counters("write"), counters("mfma")
-    bench = json.loads(open(os.path.join(SRC, "bench.json")).read().strip().splitlines()[-1])
-    m, n = bench["config"]["m"], bench["config"]["n"]
-    dt = bench["dtype"]
+    bench = [l for l in open(os.path.join(OUT, "bench_%s.log" % WL)) if l.startswith("{")][-1]
+    bench = json.loads(bench)
+    m, n, dt = bench["config"]["m"], bench["config"]["n"], bench["dtype"]
+    pdir = os.path.join(OUT, "pmc_" + WL)
+    fetch, write, busy, kname = [], [], [], None
+    for d in sorted([x for x in glob.glob(os.path.join(pdir, "fetch_size_*")) if os.path.isdir(x)]):
+        c = per_launch(d)
+        kname = dominant(c) or kname
+        if kname:
+            fetch.append(c[kname]["FETCH_SIZE"] * 1024 * 2)
+    for d in sorted([x for x in glob.glob(os.path.join(pdir, "write_size_*")) if os.path.isdir(x)]):
+        c = per_launch(d)
+        k = dominant(c)
+        if k:
+            write.append(c[k]["WRITE_SIZE"] * 1024)
+    for d in sorted([x for x in glob.glob(os.path.join(pdir, "sq_valu_mfma_busy_cycles_*")) if os.path.isdir(x)]):
+        c = per_launch(d)
+        k = dominant(c)
+        if k:
+            clk = c[k].get("GRBM_GUI_ACTIVE", 0) / 8.0      # per XCD
+            busy.append({"mfma_busy": c[k]["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * clk) if clk else None,
+                         "wait_any": c[k].get("SQ_WAIT_ANY", 0) / max(c[k].get("SQ_WAVE_CYCLES", 1), 1)})
     es = 8.0 if dt == "f64" else 4.0
     tpath = os.path.join(DST, "pmc_traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
-    lines = []
-    for k in sorted(set(fetch) | set(write)):
-        fb = fetch.get(k, {}).get("FETCH_SIZE", 0.0) * 1024 * 2
-        wb = write.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
-        lines.append("| %s | %.3g | %.3g |" % (k, fb, wb))
-        if k.startswith("k_dist_topk"):
-            traffic["m%d_n%d_p1" % (m, n) + ("" if dt == "f64" else "_" + dt)] = {
-                "kernel": k, "fetch_bytes": fb, "write_bytes": wb,
-                "hbm_bytes_per_launch": fb + wb,
-                "algorithmic_bytes_per_launch": m * n * es,
-                "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KiB->B, one launch = one full all-kNN"}
-    json.dump(traffic, open(tpath, "w"), indent=1)
-    dist = [v for k, v in mfma.items() if k.startswith("k_dist_topk")]
-    md = ["# %s profile summary: %s (%dx%d %s, k=%d, 1x MI355X)"
-          % (TAG, WL, m, n, dt, bench["config"]["k"]), "",
-          "Source: `WL=%s tools/gpu_round.sh` -> `tools/make_profiles.py %s %s`." % (WL, TAG, WL), "",
-          "## bench.py line", "", "```json", json.dumps(bench), "```", "",
-          "## PMC traffic per launch (bytes)", "", "| kernel | fetch (x2) | write |", "|---|---|---|"]
-    md += lines
-    if dist:
-        d = dist[0]
-        clk = d.get("GRBM_GUI_ACTIVE", 0) / 8.0
-        md += ["", "## k_dist_topk utilisation", "",
-               "- GRBM_GUI_ACTIVE/8 = %.4g cycles per XCD" % clk,
-               "- SQ_VALU_MFMA_BUSY_CYCLES = %.4g (/(1024 SIMDs x GRBM/8) = %.1f%% MFMA busy)"
-               % (d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0),
-                  100.0 * d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (1024 * clk) if clk else 0),
-               "- SQ_WAIT_ANY / SQ_WAVE_CYCLES = %.1f%%"
-               % (100.0 * d.get("SQ_WAIT_ANY", 0) / max(d.get("SQ_WAVE_CYCLES", 1), 1))]
+    key = "m%d_n%d_p1" % (m, n) + ("" if dt == "f64" else "_" + dt)
+    if WL == "mnist-real":
+        key += "_real"
+    rec = None
+    if fetch and write:
+        f, w = statistics.median(fetch), statistics.median(write)
+        rec = {"kernel": kname, "fetch_bytes": f, "write_bytes": w, "hbm_bytes_per_launch": f + w,
+               "samples_fetch_bytes": fetch, "samples_write_bytes": write,
+               "algorithmic_bytes_per_launch": m * n * es,
+               "note": "median of %d passes; FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KiB->B, one launch = "
+                       "one full all-kNN (%s %s)" % (len(fetch), TAG, WL)}
+        traffic[key] = rec
+        json.dump(traffic, open(tpath, "w"), indent=1)
+    md = ["# %s profile summary: %s (%dx%d %s, k=%d, 1x MI355X)" % (TAG, WL, m, n, dt, bench["config"]["k"]),
+          "", "Source: `tools/gpu.sh bench:%s trace:%s pmc:%s:%d` -> `tools/make_profiles.py %s %s`."
+          % (WL, WL, WL, len(fetch), TAG, WL), "", "## bench.py line", "", "```json", json.dumps(bench), "```", ""]
+    if rec:
+        md += ["## PMC traffic of %s per launch (bytes, median of %d passes)" % (kname, len(fetch)), "",
+               "| | median | min | max |", "|---|---|---|---|",
+               "| FETCH_SIZE x2 | %.4g | %.4g | %.4g |" % (rec["fetch_bytes"], min(fetch), max(fetch)),
+               "| WRITE_SIZE | %.4g | %.4g | %.4g |" % (rec["write_bytes"], min(write), max(write)),
+               "| algorithmic (corpus bytes) | %.4g | | |" % rec["algorithmic_bytes_per_launch"], ""]
+    if busy:
+        mb = [b["mfma_busy"] for b in busy if b["mfma_busy"] is not None]
+        wa = [b["wait_any"] for b in busy]
+        md += ["## %s utilisation (%d passes)" % (kname, len(busy)), "",
+               "- MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8): median %.1f%% "
+               "(%.1f..%.1f)" % (100 * statistics.median(mb), 100 * min(mb), 100 * max(mb)),
+               "- SQ_WAIT_ANY / SQ_WAVE_CYCLES: median %.1f%%" % (100 * statistics.median(wa))]
     open(os.path.join(DST, "%s_%s_summary.md" % (TAG, WL)), "w").write("\n".join(md) + "\n")
     print("\n".join(md))
 
