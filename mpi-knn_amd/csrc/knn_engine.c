@@ -88,6 +88,7 @@ struct knn_ctx {
     int nsplit_last;
     size_t split_nc;    /* choose_splits cache: corpus rows -> split count */
     int split_lpq;
+    int split_i8;     /* the cached choice was made for the int8 kernel */
     int split_best;
     int nfail;
     int mode;
@@ -575,15 +576,21 @@ static size_t split_bytes(const knn_ctx_t *c)
  * list-scheduling bound instead of the simulation. */
 #define KNN_XCDS 8
 #define KNN_WG_COST 0.5        /* prologue + partial-list flush, in tiles   */
+/* int8 kernel: a workgroup's fixed cost (query fragments into VGPRs, ring
+ * fill, warming 512 empty lane lists, the flush) is ~60 K-step tiles'
+ * worth: tile time scales with the K-steps, the fixed cost does not.
+ * Calibrated on the emulated ring (tools/ring_emulate.py, KNN_SPLITS sweeps):
+ * mnist P = 2 / 4 / 8 best at 1-3 / 1-2 / 4 splits, sift P = 4 / 8 at 1. */
+#define KNN_WG_COST_I8_KSTEPS 60.0
 #define KNN_MERGE_COST 1e-6    /* k_merge per (query, split), in tiles      */
-static double launch_makespan(long nqb, long ntiles, int s, int cus)
+static double launch_makespan(long nqb, long ntiles, int s, int cus, double wgc)
 {
     const long tb = ntiles / s, tr = ntiles % s;
     const long w = nqb * s;
     const int per = cus / KNN_XCDS > 0 ? cus / KNN_XCDS : 1;
     if (w > 16L * cus || per > 64) {
-        const double work = (double)nqb * ntiles + KNN_WG_COST * w;
-        return work / cus + (tb + (tr ? 1 : 0)) + KNN_WG_COST;
+        const double work = (double)nqb * ntiles + wgc * w;
+        return work / cus + (tb + (tr ? 1 : 0)) + wgc;
     }
     double ms = 0.0;
     for (int x = 0; x < KNN_XCDS; x++) {
@@ -593,7 +600,7 @@ static double launch_makespan(long nqb, long ntiles, int s, int cus)
             int best = 0;
             for (int u = 1; u < per; u++)
                 if (cu[u] < cu[best]) best = u;
-            cu[best] += (double)(tb + (split < tr ? 1 : 0)) + KNN_WG_COST;
+            cu[best] += (double)(tb + (split < tr ? 1 : 0)) + wgc;
         }
         for (int u = 0; u < per; u++)
             if (cu[u] > ms) ms = cu[u];
@@ -614,16 +621,18 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         int s = atoi(env);
         return s > KNN_MAX_LISTS / c->lpq ? KNN_MAX_LISTS / c->lpq : s;
     }
-    if (c->split_nc == nc && c->split_lpq == c->lpq && c->split_best > 0) return c->split_best;
+    if (c->split_nc == nc && c->split_lpq == c->lpq && c->split_i8 == c->i8 && c->split_best > 0)
+        return c->split_best;
     int smax = KNN_MAX_LISTS / c->lpq;
     const size_t per = split_bytes(c);
     if (per > 0 && KNN_PART_BUDGET / per < (size_t)smax)
         smax = KNN_PART_BUDGET / per > 1 ? (int)(KNN_PART_BUDGET / per) : 1;
+    const double wgc = c->i8 ? KNN_WG_COST_I8_KSTEPS / (double)(knn_s8_rs(c->n) / 32) : KNN_WG_COST;
     int best = 1;
     double best_t = 0.0;
     for (int s = 1; s <= smax; s++) {
         if (s > 1 && ntiles / s < 4) break;
-        const double t = launch_makespan(nqb, ntiles, s, c->cus) +
+        const double t = launch_makespan(nqb, ntiles, s, c->cus, wgc) +
                          KNN_MERGE_COST * (double)c->nq * s;
         if (s == 1 || t < best_t * (1.0 - 2e-3)) {
             best = s;
@@ -632,6 +641,7 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     }
     c->split_nc = nc;
     c->split_lpq = c->lpq;
+    c->split_i8 = c->i8;
     c->split_best = best;
     return best;
 }

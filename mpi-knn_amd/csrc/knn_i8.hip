@@ -402,6 +402,21 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                     if (!(row0 + rloc + 4 * h < nc && idb + rloc != gq)) pend &= ~(1u << x);
                 }
             }
+            // one survivor at most in every lane (the common case once the
+            // bounds are tight) and no buffer filling up: the survivor is the
+            // lane minimum, so no select tree and no merge (a second merge
+            // site costs ~34 VGPRs)
+            const bool one = G == MB && !masked &&
+                             __ballot(__popc(pend) > 1 || (pend != 0 && cnt == NB - 1)) == 0ull;
+            if (one) {
+                if (pend) {
+                    const int x = __builtin_ctz(pend), r = x & 15;
+                    bk[64 * cnt] = lmn + qn;
+                    bi[64 * cnt] = idb + 32 * (x >> 4) + 8 * (r >> 2) + (r & 3);
+                    cnt++;
+                }
+                pend = 0;
+            }
             while (__ballot(pend != 0) != 0ull) {
                 const int x = pend ? __builtin_ctz(pend) : 0;
                 int v[8 * G];

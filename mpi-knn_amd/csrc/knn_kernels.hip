@@ -806,7 +806,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
 // new in this step get their exact reference-order S from the resident
 // block (the only step at which their rows are on this device).
 // ---------------------------------------------------------------------------
-template <typename TE, int KP>
+template <typename TE, int KP, int S>
 __global__ __launch_bounds__(256) void k_merge(
     const double *__restrict__ part_d, const int *__restrict__ part_i,
     const double *__restrict__ part_T, int nsplit, int lpq, int kl, int nq, int nq_pad, int first_step,
@@ -815,22 +815,30 @@ __global__ __launch_bounds__(256) void k_merge(
     const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
     const double *__restrict__ meta, int k, unsigned long long *__restrict__ qthr)
 {
+    // S lanes a query (64, or 32 when nl + 1 <= 32: two queries a wave, so
+    // twice the independent argmin chains a SIMD interleaves -- the merge is
+    // bound by the latency of its KP + 1 dependent rounds, not by issue)
+    constexpr int QPW = 64 / S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int q = blockIdx.x * 4 + wave;
-    if (q >= nq) return;
+    const int seg = lane / S, sl = lane - seg * S;
+    const int q0 = (blockIdx.x * 4 + wave) * QPW;
+    if (q0 >= nq) return;
+    const int q = q0 + seg;
+    const bool qv = q < nq;
+    const unsigned long long segm = (S == 64) ? ~0ull : (0xffffffffull << (32 * seg));
     const int mode = knn_mode<TE>(meta, n);
     const int nl = lpq * nsplit;   // partial lists: [split][query][lpq][kl]
 
     const double *src_d = nullptr;
     const int *src_i = nullptr;
     int len = KP;
-    if (lane < nl) {
-        const int s = lane / lpq, gg = lane - s * lpq;
+    if (qv && sl < nl) {
+        const int s = sl / lpq, gg = sl - s * lpq;
         const size_t base = (((size_t)s * nq_pad + q) * lpq + gg) * kl;
         src_d = part_d + base;
         src_i = part_i + base;
         len = kl;
-    } else if (lane == nl && !first_step) {
+    } else if (qv && sl == nl && !first_step) {
         src_d = st_d + (size_t)q * KP;
         src_i = st_i + (size_t)q * KP;
     }
@@ -844,15 +852,15 @@ __global__ __launch_bounds__(256) void k_merge(
     // after every kept entry by (d^2, idx), so only the GEMM certificate
     // needs them).
     double T = KNN_INF, Td = KNN_INF;
-    if (lane < nsplit) T = part_T[(size_t)lane * nq_pad + q];
-    if (lane == nl && !first_step) { T = st_T[2 * (size_t)q]; Td = st_T[2 * (size_t)q + 1]; }
-    for (int off = 32; off > 0; off >>= 1) {
+    if (qv && sl < nsplit) T = part_T[(size_t)sl * nq_pad + q];
+    if (qv && sl == nl && !first_step) { T = st_T[2 * (size_t)q]; Td = st_T[2 * (size_t)q + 1]; }
+    for (int off = S / 2; off > 0; off >>= 1) {
         T = fmin(T, __shfl_xor(T, off));
         Td = fmin(Td, __shfl_xor(Td, off));
     }
 
-    // state slot r (0..KP-1) is kept by lane r & 63 in its register r >> 6
-    constexpr int NS = (KP + 63) / 64;
+    // state slot r (0..KP-1) is kept by segment lane r % S in register r / S
+    constexpr int NS = (KP + S - 1) / S;
     double sd[NS];
     int si[NS], ssrc[NS], spos[NS];
 #pragma unroll
@@ -860,31 +868,41 @@ __global__ __launch_bounds__(256) void k_merge(
     for (int r = 0; r <= KP; r++) {
         double wd = hd;
         int wi = hi;
-        wave_argmin(wd, wi);
-        if (wd == KNN_INF) break;  // every remaining head is empty
-        const unsigned long long who = __ballot(hd == wd && hi == wi);
-        const int wl = __builtin_ctzll(who);
-        const int wpos = __shfl(pos, wl);
-        if (r < KP) {
-            if (lane == (r & 63)) {
 #pragma unroll
-                for (int x = 0; x < NS; x++) {
-                    if ((r >> 6) == x) {
-                        sd[x] = wd;
-                        si[x] = wi;
-                        ssrc[x] = (wl == nl && !first_step) ? 1 : 0;
-                        spos[x] = wpos;
+        for (int off = S / 2; off > 0; off >>= 1) {
+            const double od = __shfl_xor(wd, off);
+            const int oi = __shfl_xor(wi, off);
+            const bool take = (od < wd) || (od == wd && oi < wi);
+            wd = take ? od : wd;
+            wi = take ? oi : wi;
+        }
+        const bool live = wd != KNN_INF;   // this query still has heads
+        if (__ballot(live) == 0ull) break;
+        const unsigned long long who = __ballot(live && hd == wd && hi == wi) & segm;
+        const int wl = who ? __builtin_ctzll(who) : lane;   // wave lane of the winner
+        const int wpos = __shfl(pos, wl);
+        if (live) {
+            if (r < KP) {
+                if (sl == r % S) {
+#pragma unroll
+                    for (int x = 0; x < NS; x++) {
+                        if (r / S == x) {
+                            sd[x] = wd;
+                            si[x] = wi;
+                            ssrc[x] = (wl - seg * S == nl && !first_step) ? 1 : 0;
+                            spos[x] = wpos;
+                        }
                     }
                 }
+            } else {
+                Td = fmin(Td, wd);
             }
-        } else {
-            Td = fmin(Td, wd);
-        }
-        if (lane == wl) {
-            pos++;
-            hd = (pos < len) ? src_d[pos] : KNN_INF;
-            hi = (pos < len) ? src_i[pos] : 0x7fffffff;
-            if (hd == KNN_INF) hi = 0x7fffffff;
+            if (lane == wl) {
+                pos++;
+                hd = (pos < len) ? src_d[pos] : KNN_INF;
+                hi = (pos < len) ? src_i[pos] : 0x7fffffff;
+                if (hd == KNN_INF) hi = 0x7fffffff;
+            }
         }
     }
 
@@ -898,17 +916,17 @@ __global__ __launch_bounds__(256) void k_merge(
     if (qthr != nullptr && mode == KNN_MODE_INT) {
         int z = 0;
 #pragma unroll
-        for (int x = 0; x < NS; x++) z += __popcll(__ballot(lane + 64 * x < KP && sd[x] == 0.0));
+        for (int x = 0; x < NS; x++) z += __popcll(__ballot(sl + S * x < KP && sd[x] == 0.0) & segm);
         const int rk = k + z;
         if (rk < KP) {
             double u = KNN_INF;
 #pragma unroll
             for (int x = 0; x < NS; x++) {
-                const double v = __shfl(sd[x], rk & 63);
-                if ((rk >> 6) == x) u = v;
+                const double v = __shfl(sd[x], seg * S + rk % S);
+                if (rk / S == x) u = v;
             }
             if constexpr (sizeof(TE) == 4) u = (double)__double2float_ru(u);
-            if (lane == 0 && u < KNN_INF)
+            if (qv && sl == 0 && u < KNN_INF)
                 atomicMin(qthr + q, (unsigned long long)__double_as_longlong(u));
         }
     }
@@ -921,17 +939,17 @@ __global__ __launch_bounds__(256) void k_merge(
     // the top k: its S is skipped and marked +inf (k_finalize ignores it).
     double win = KNN_INF;
     if (mode == KNN_MODE_GEMM) {
-        const double E = knn_cert_E<TE>(n, (double)qblk[qnorm_off + q], meta[KNN_META_MAXNORM]);
+        const double E = qv ? knn_cert_E<TE>(n, (double)qblk[qnorm_off + q], meta[KNN_META_MAXNORM]) : 0.0;
         int z = 0;
 #pragma unroll
-        for (int x = 0; x < NS; x++) z += __popcll(__ballot(lane + 64 * x < KP && sd[x] <= E));
+        for (int x = 0; x < NS; x++) z += __popcll(__ballot(sl + S * x < KP && sd[x] <= E) & segm);
         const int rk = k - 1 + z;
         double dk = KNN_INF;
         if (rk < KP) {
 #pragma unroll
             for (int x = 0; x < NS; x++) {
-                const double v = __shfl(sd[x], rk & 63);
-                if ((rk >> 6) == x) dk = v;
+                const double v = __shfl(sd[x], seg * S + rk % S);
+                if (rk / S == x) dk = v;
             }
         }
         if (dk < KNN_INF) win = (dk + 2.0 * E) * (1.0 + 1.0 / 1048576.0);
@@ -940,7 +958,7 @@ __global__ __launch_bounds__(256) void k_merge(
 #pragma unroll
     for (int x = 0; x < NS; x++) {
         sx[x] = sd[x];
-        if (lane + 64 * x < KP && mode == KNN_MODE_GEMM && si[x] >= 0) {
+        if (qv && sl + S * x < KP && mode == KNN_MODE_GEMM && si[x] >= 0) {
             if (ssrc[x]) {
                 sx[x] = st_x[(size_t)q * KP + spos[x]];
             } else if (sd[x] <= win) {
@@ -952,18 +970,20 @@ __global__ __launch_bounds__(256) void k_merge(
         }
     }
     // every read of the old state (any lane, any slot) completes before the
-    // first write (wave-private query)
+    // first write (wave-private queries)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (qv) {
 #pragma unroll
-    for (int x = 0; x < NS; x++) {
-        const int r = lane + 64 * x;
-        if (r < KP) {
-            st_d[(size_t)q * KP + r] = sd[x];
-            st_x[(size_t)q * KP + r] = sx[x];
-            st_i[(size_t)q * KP + r] = (sd[x] == KNN_INF) ? -1 : si[x];
+        for (int x = 0; x < NS; x++) {
+            const int r = sl + S * x;
+            if (r < KP) {
+                st_d[(size_t)q * KP + r] = sd[x];
+                st_x[(size_t)q * KP + r] = sx[x];
+                st_i[(size_t)q * KP + r] = (sd[x] == KNN_INF) ? -1 : si[x];
+            }
         }
+        if (sl == 0) { st_T[2 * (size_t)q] = T; st_T[2 * (size_t)q + 1] = Td; }
     }
-    if (lane == 0) { st_T[2 * (size_t)q] = T; st_T[2 * (size_t)q + 1] = Td; }
     (void)nc;
 }
 
@@ -1623,13 +1643,21 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
     if (lpq < 1 || kl < 1 || lpq * nsplit + 1 > 64 || k <= 0 || k > kp) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
     const size_t qn_off = q_rows_pad * (size_t)np;
-    const dim3 grid((unsigned)((nq + 3) / 4));
+    // two queries a wave when their lists and state fit 32 lanes
+    const int two = lpq * nsplit + 1 <= 32;
+    const dim3 grid((unsigned)((nq + (two ? 7 : 3)) / (two ? 8 : 4)));
     hipStream_t s = (hipStream_t)stream;
-#define CALL(T, KL, KP)                                                                         \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP>), grid, dim3(256), 0, s, part_d, part_i,    \
-                       part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x, st_i, st_T,   \
-                       (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n, np, meta, k,       \
-                       (unsigned long long *)qthr);                                              \
+#define CALL(T, KL, KP)                                                                          \
+    if (two)                                                                                     \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP, 32>), grid, dim3(256), 0, s, part_d,     \
+                           part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
+                           st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
+                           np, meta, k, (unsigned long long *)qthr);                               \
+    else                                                                                         \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP, 64>), grid, dim3(256), 0, s, part_d,     \
+                           part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
+                           st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
+                           np, meta, k, (unsigned long long *)qthr);                               \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
