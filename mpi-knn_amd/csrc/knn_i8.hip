@@ -251,6 +251,11 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         const double td = __longlong_as_double((long long)atomicMin(qthr + myq, 0x7ff0000000000000ull));
         thr = td >= 2147483647.0 ? I8_INF : (int)td;
     }
+    // padding queries of the last block (myq >= nq) reject every candidate:
+    // with an open bound their lanes took the insertion path for every row,
+    // and the one workgroup holding them set the launch's span (a 7500-row
+    // ring step: 134 us against a 74 us average workgroup)
+    if (myq >= nq) thr = -1;
     // vmcnt(0) through the builtin: hipcc's wait pass then knows the query
     // loads are complete (an asm wait would leave it inserting vmcnt(N)
     // before each later use of qf, draining the LDS-DMA ring)

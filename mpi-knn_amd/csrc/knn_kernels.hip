@@ -389,6 +389,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     T thr = (T)KNN_INF;
     if (qthr != nullptr && myq < nq)
         thr = (T)__longlong_as_double((long long)atomicMin(qthr + myq, 0x7ff0000000000000ull));
+    if (myq >= nq) thr = -(T)KNN_INF;   // padding queries reject every candidate
     asm volatile("" ::"v"(thr));
 
     const int total = (mode == KNN_MODE_SCAN || t_hi <= t_lo) ? 0 : (t_hi - t_lo) * nfc;
