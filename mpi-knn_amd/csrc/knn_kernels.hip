@@ -213,20 +213,41 @@ __global__ __launch_bounds__(256) void k_norms(T *__restrict__ blk, size_t rows,
     double *meta = (double *)(norms + rows_pad);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double mabs = 0.0, mnorm = 0.0, nonint = 0.0, nonfin = 0.0, mpos = 0.0, mneg = 0.0;
+    // 16-byte loads (rows are whole 128-byte chunks, zero past n), four in
+    // flight a lane: the pass is bound by load latency, not by its ALU work
+    typedef typename std::conditional<sizeof(T) == 8, dbl2, flt4>::type vec_t;
+    constexpr int V = 16 / (int)sizeof(T);
+    auto acc = [&](double v, double &s) {
+        s = fma(v, v, s);
+        if (!__builtin_isfinite(v)) nonfin = 1.0;
+        else {
+            const double a = fabs(v);
+            mabs = a > mabs ? a : mabs;
+            mpos = v > mpos ? v : mpos;
+            mneg = -v > mneg ? -v : mneg;
+            if (v != rint(v)) nonint = 1.0;
+        }
+    };
     for (size_t i = (size_t)blockIdx.x * 4 + wave; i < rows_pad; i += (size_t)gridDim.x * 4) {
-        const T *x = blk + i * n_pad;
+        const vec_t *x = (const vec_t *)(blk + i * n_pad);
         double s = 0.0;
         if (i < rows) {
-            for (int j = lane; j < n; j += 64) {
-                double v = (double)x[j];
-                s = fma(v, v, s);
-                if (!__builtin_isfinite(v)) nonfin = 1.0;
-                else {
-                    double a = fabs(v);
-                    mabs = a > mabs ? a : mabs;
-                    mpos = v > mpos ? v : mpos;
-                    mneg = -v > mneg ? -v : mneg;
-                    if (v != rint(v)) nonint = 1.0;
+            const int nv = n_pad / V;              // whole vectors a row
+            for (int j0 = lane; j0 < nv; j0 += 4 * 64) {
+                vec_t w[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int j = j0 + 64 * u;
+                    if (j < nv) w[u] = x[j];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int j = j0 + 64 * u;
+                    if (j < nv) {
+#pragma unroll
+                        for (int e = 0; e < V; e++)
+                            if (j * V + e < n) acc((double)w[u][e], s);
+                    }
                 }
             }
         }
