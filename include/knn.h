@@ -256,6 +256,15 @@ KNN_API int knn_ctx_step_shadow(knn_ctx_t *ctx, const void *d_sblock, size_t nc,
                                 void *stream);
 KNN_API int knn_ctx_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
                  size_t c_base, void *stream);
+/* Fold nblk resident shadow-form blocks (d_sblocks[b]: nc[b] rows, global
+ * ids c_base[b]..; any order) -- the direct-exchange ring's step over every
+ * block received from the other ranks (blk:217-242 for all of them at
+ * once).  Byte blocks (knn_ctx_shadow == 2) share one distance launch per 8
+ * blocks, which counts as ONE step of the lag rule above: none of the
+ * blocks may be overwritten before KNN_STEP_LAG further steps (or
+ * knn_ctx_end).  fp16 shadow blocks fold one block a step. */
+KNN_API int knn_ctx_step_shadow_n(knn_ctx_t *ctx, int nblk, const void *const *d_sblocks,
+                                  const size_t *nc, const size_t *c_base, void *stream);
 
 /* Finish: write nq*k records to d_out.  Returns in *unresolved (host; the
  * call synchronises the stream) the number of queries whose candidate set

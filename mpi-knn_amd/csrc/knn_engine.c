@@ -86,10 +86,12 @@ struct knn_ctx {
     const double *meta;
     int first_step;
     int nsplit_last;
-    size_t split_nc;    /* choose_splits cache: corpus rows -> split count */
-    int split_lpq;
-    int split_i8;     /* the cached choice was made for the int8 kernel */
-    int split_best;
+    /* choose_splits cache: (corpus rows, list shape, kernel) -> split count;
+     * a direct-exchange pass alternates two launch sizes, and one model
+     * evaluation costs ~0.5 ms of host time at 15000 queries */
+#define KNN_SPLIT_CACHE 8
+    struct { size_t nc; int lpq, i8, best; } split_cache[KNN_SPLIT_CACHE];
+    int split_next;
     int nfail;
     int mode;
     /* kernel timing (knn_ctx_profile): 3 events per step bracket
@@ -583,6 +585,10 @@ static size_t split_bytes(const knn_ctx_t *c)
  * mnist P = 2 / 4 / 8 best at 1-3 / 1-2 / 4 splits, sift P = 4 / 8 at 1. */
 #define KNN_WG_COST_I8_KSTEPS 60.0
 #define KNN_MERGE_COST 1e-6    /* k_merge per (query, split), in tiles      */
+/* int8 kernel: k_merge's exposed time grows ~1.2e-4 tile times per (query,
+ * split) (emulated P = 8 fused launch: 13 splits 0.10 ms against 4 splits
+ * 0.06 ms of exposed merge at 7500 queries) */
+#define KNN_MERGE_COST_I8 1.2e-4
 static double launch_makespan(long nqb, long ntiles, int s, int cus, double wgc)
 {
     const long tb = ntiles / s, tr = ntiles % s;
@@ -621,28 +627,42 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         int s = atoi(env);
         return s > KNN_MAX_LISTS / c->lpq ? KNN_MAX_LISTS / c->lpq : s;
     }
-    if (c->split_nc == nc && c->split_lpq == c->lpq && c->split_i8 == c->i8 && c->split_best > 0)
-        return c->split_best;
+    for (int e = 0; e < KNN_SPLIT_CACHE; e++)
+        if (c->split_cache[e].best > 0 && c->split_cache[e].nc == nc && c->split_cache[e].lpq == c->lpq &&
+            c->split_cache[e].i8 == c->i8)
+            return c->split_cache[e].best;
     int smax = KNN_MAX_LISTS / c->lpq;
     const size_t per = split_bytes(c);
     if (per > 0 && KNN_PART_BUDGET / per < (size_t)smax)
         smax = KNN_PART_BUDGET / per > 1 ? (int)(KNN_PART_BUDGET / per) : 1;
     const double wgc = c->i8 ? KNN_WG_COST_I8_KSTEPS / (double)(knn_s8_rs(c->n) / 32) : KNN_WG_COST;
-    int best = 1;
+    const double mc = c->i8 ? KNN_MERGE_COST_I8 : KNN_MERGE_COST;
+    /* int8 lists: at least s_min splits so that a lane list expects <= KL/4
+     * of the query's k+1 nearest (lpq lists a split; the block may hold all
+     * of them): one split of 17-entry lists over a whole corpus left
+     * ~1e-3 of the queries uncertified (a lane list held 17 of the k) */
+    int s_min = 1;
+    if (c->i8) {
+        const int kl = knn_i8_kl(c->kp);
+        s_min = (4 * (c->k + 1) + c->lpq * kl - 1) / (c->lpq * kl);
+        if (s_min > smax) s_min = smax;
+        if (s_min < 1) s_min = 1;
+    }
+    int best = s_min;
     double best_t = 0.0;
-    for (int s = 1; s <= smax; s++) {
-        if (s > 1 && ntiles / s < 4) break;
-        const double t = launch_makespan(nqb, ntiles, s, c->cus, wgc) +
-                         KNN_MERGE_COST * (double)c->nq * s;
-        if (s == 1 || t < best_t * (1.0 - 2e-3)) {
+    for (int s = s_min; s <= smax; s++) {
+        if (s > s_min && ntiles / s < 4) break;
+        const double t = launch_makespan(nqb, ntiles, s, c->cus, wgc) + mc * (double)c->nq * s;
+        if (s == s_min || t < best_t * (1.0 - 2e-3)) {
             best = s;
             best_t = t;
         }
     }
-    c->split_nc = nc;
-    c->split_lpq = c->lpq;
-    c->split_i8 = c->i8;
-    c->split_best = best;
+    const int e = c->split_next++ % KNN_SPLIT_CACHE;
+    c->split_cache[e].nc = nc;
+    c->split_cache[e].lpq = c->lpq;
+    c->split_cache[e].i8 = c->i8;
+    c->split_cache[e].best = best;
     return best;
 }
 
@@ -737,11 +757,40 @@ static int merge_pending(knn_ctx_t *c)
  * enqueues after step s returns is ordered after step s-2 only, so a ring
  * rotates KNN_STEP_LAG + 2 receive buffers (knn.h).  knn_ctx_end joins
  * all. */
-/* d_sblock: a shadow block (knn_shadow_pack) used in place of d_cblock */
+/* d_sblock: a shadow block (knn_shadow_pack) used in place of d_cblock.
+ * xb (int8 contraction only, byte blocks): further byte blocks folded by the
+ * same launch -- xb->ptr[0..nblk) with the rows / bases beside them, in any
+ * order (sorted here); d_sblock / nc / c_base then unused. */
 static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sblock, size_t nc,
-                         size_t c_base, void *stream)
+                         size_t c_base, const knn_i8_blocks_t *xb, void *stream)
 {
-    if (!c || !(d_cblock || d_sblock) || nc == 0 || nc > c->block_cap) return KNN_ERR_INVALID;
+    knn_i8_blocks_t tab;
+    memset(&tab, 0, sizeof(tab));
+    if (xb) {
+        if (!c || !c->i8 || xb->nblk < 1 || xb->nblk > KNN_I8_MAXBLK) return KNN_ERR_INVALID;
+        /* ascending bases (insertion sort, <= 8 entries) */
+        for (int b = 0; b < xb->nblk; b++) {
+            if (!xb->ptr[b] || xb->nc[b] <= 0 || (size_t)xb->nc[b] > c->block_cap || xb->base[b] < 0)
+                return KNN_ERR_INVALID;
+            int j = tab.nblk++;
+            while (j > 0 && tab.base[j - 1] > xb->base[b]) {
+                tab.ptr[j] = tab.ptr[j - 1];
+                tab.base[j] = tab.base[j - 1];
+                tab.nc[j] = tab.nc[j - 1];
+                j--;
+            }
+            tab.ptr[j] = xb->ptr[b];
+            tab.base[j] = xb->base[b];
+            tab.nc[j] = xb->nc[b];
+        }
+        d_sblock = tab.ptr[0];
+        c_base = (size_t)tab.base[0];
+        nc = 0;   /* tile-rounded rows of the launch: the split model's input */
+        for (int b = 0; b < tab.nblk; b++) nc += knn_round_up((size_t)tab.nc[b], KNN_TC);
+        nc -= knn_round_up((size_t)tab.nc[tab.nblk - 1], KNN_TC) - (size_t)tab.nc[tab.nblk - 1];
+    } else if (!c || !(d_cblock || d_sblock) || nc == 0 || nc > c->block_cap) {
+        return KNN_ERR_INVALID;
+    }
     if (d_sblock && !c->shadow) return KNN_ERR_INVALID;
     if (!d_cblock) d_cblock = d_sblock;   /* INT mode: k_merge never reads its rows */
     HIPCHK(hipSetDevice(c->device));
@@ -755,9 +804,16 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     const char *np_env = getenv("KNN_NO_PAIR");
     const int can_pair = (c->h16 || c->i8) && 2 * c->lpq * nsplit + 1 <= 64 &&
                          !(np_env && np_env[0] == '1');
+    /* a fused step (the direct exchange's received blocks) starts after the
+     * previous step's merge: that merge publishes the (k+1)-th d^2 of the
+     * blocks folded so far into qthr, so the fused launch -- most of the
+     * rank's work -- filters with it from its first tile instead of
+     * warming every lane list cold (KNN_FUSE_WAIT=0: no wait) */
+    const char *fw_env = getenv("KNN_FUSE_WAIT");
+    const int fuse_wait = xb && c->nstep > 0 && !(fw_env && fw_env[0] == '0');
     int pairing = 0;
     if ((set & 1) && c->pend) {
-        pairing = can_pair && nsplit == c->pend_nsplit;
+        pairing = can_pair && nsplit == c->pend_nsplit && !fuse_wait;
         if (!pairing) RCHK(merge_pending(c));
     }
     {
@@ -776,6 +832,10 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     HIPCHK(hipEventRecord(c->ev_in, cs));
     HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
     if (c->nstep >= KNN_PSETS) HIPCHK(hipStreamWaitEvent(ds, c->ev_m[set], 0));
+    if (fuse_wait) {
+        if (c->pend) RCHK(merge_pending(c));   /* (pending only at an even set) */
+        HIPCHK(hipStreamWaitEvent(ds, c->ev_m[(c->nstep - 1) % KNN_PSETS], 0));
+    }
     const void *csh = d_sblock, *cn_ptr = NULL;
     if (c->i8) {
         if (!d_sblock && d_cblock == c->qblk && knn_rows_pad(c->block_cap) == c->q_rows_pad) {
@@ -806,12 +866,17 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
         ev = &c->prof_ev[3 * c->prof_pending++];
         HIPCHK(hipEventRecord(ev[0], ds));
     }
-    if (c->i8)
-        RCHK(knn_launch_dist_i8(c->kp, c->k, c->qs8, c->q_rows_pad, c->q_base, (int)c->nq, csh,
-                                knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, nsplit,
-                                c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad,
-                                c->qthr, ds));
-    else
+    if (c->i8) {
+        if (!xb) {
+            tab.nblk = 1;
+            tab.ptr[0] = csh;
+            tab.base[0] = (int64_t)c_base;
+            tab.nc[0] = (int)nc;
+        }
+        RCHK(knn_launch_dist_i8(c->kp, c->k, c->qs8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
+                                knn_rows_pad(c->block_cap), (int)c->n, nsplit, c->part_d[set],
+                                c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr, ds));
+    } else
         RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq,
                                   cblk, knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta,
                                   nsplit, c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad,
@@ -856,13 +921,41 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
 
 int knn_ctx_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base, void *stream)
 {
-    return ctx_step_impl(c, d_cblock, NULL, nc, c_base, stream);
+    return ctx_step_impl(c, d_cblock, NULL, nc, c_base, NULL, stream);
 }
 
 int knn_ctx_step_shadow(knn_ctx_t *c, const void *d_sblock, size_t nc, size_t c_base, void *stream)
 {
     if (!d_sblock) return KNN_ERR_INVALID;
-    return ctx_step_impl(c, NULL, d_sblock, nc, c_base, stream);
+    return ctx_step_impl(c, NULL, d_sblock, nc, c_base, NULL, stream);
+}
+
+/* Several resident blocks in one step: byte blocks (knn_ctx_shadow == 2)
+ * share one k_dist_topk_i8 launch per KNN_I8_MAXBLK blocks -- one launch's
+ * fixed cost and one cold start instead of one per block, and splits long
+ * enough to fill the CUs at P = 8; other forms fold one block a step. */
+int knn_ctx_step_shadow_n(knn_ctx_t *c, int nblk, const void *const *d_sblocks, const size_t *nc,
+                          const size_t *c_base, void *stream)
+{
+    if (!c || nblk < 1 || !d_sblocks || !nc || !c_base || !c->shadow) return KNN_ERR_INVALID;
+    for (int b = 0; b < nblk; b++)
+        if (!d_sblocks[b] || nc[b] == 0 || nc[b] > c->block_cap) return KNN_ERR_INVALID;
+    if (c->shadow != 2 || env_on("KNN_NO_FUSE")) {
+        for (int b = 0; b < nblk; b++) RCHK(ctx_step_impl(c, NULL, d_sblocks[b], nc[b], c_base[b], NULL, stream));
+        return KNN_OK;
+    }
+    for (int b0 = 0; b0 < nblk; b0 += KNN_I8_MAXBLK) {
+        knn_i8_blocks_t xb;
+        memset(&xb, 0, sizeof(xb));
+        xb.nblk = nblk - b0 < KNN_I8_MAXBLK ? nblk - b0 : KNN_I8_MAXBLK;
+        for (int b = 0; b < xb.nblk; b++) {
+            xb.ptr[b] = d_sblocks[b0 + b];
+            xb.nc[b] = (int)nc[b0 + b];
+            xb.base[b] = (int64_t)c_base[b0 + b];
+        }
+        RCHK(ctx_step_impl(c, NULL, NULL, 0, 0, &xb, stream));
+    }
+    return KNN_OK;
 }
 
 int knn_ctx_shadow(const knn_ctx_t *c) { return c ? c->shadow : 0; }

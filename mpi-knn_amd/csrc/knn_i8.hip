@@ -94,6 +94,15 @@ __device__ __forceinline__ void bglds16x2(knn_v4i rsrc, unsigned v0, unsigned v1
                  : "memory", "scc");
 }
 
+// buffer descriptor of a wave-uniform base, pinned to SGPRs (the base comes
+// from the LDS block table through readfirstlane; under register pressure
+// the allocator otherwise left the descriptor in VGPRs)
+__device__ __forceinline__ knn_v4i i8_rsrc(const void *base)
+{
+    const knn_v4i r = knn_rsrc(base);
+    return (knn_v4i){__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y), r.z, r.w};
+}
+
 // a where the lane's bit of m is clear, b where it is set
 __device__ __forceinline__ int i8_sel(unsigned long long m, int a, int b)
 {
@@ -151,6 +160,33 @@ __global__ __launch_bounds__(256) void k_shadow8(signed char *__restrict__ dst, 
     }
 }
 
+// Block table of the launch in LDS (written once by thread 0 from the
+// kernel argument with static indices, so the argument is never indexed
+// dynamically and its SGPRs die after the copy).  Lookups happen once a
+// block (wave-uniform LDS reads, made scalar by readfirstlane).
+struct i8_tab_lds {
+    unsigned long long ptr[KNN_I8_MAXBLK];
+    long long base[KNN_I8_MAXBLK];
+    int nc[KNN_I8_MAXBLK];
+    int t0[KNN_I8_MAXBLK + 1];
+    int nblk;
+};
+__device__ __forceinline__ int i8_rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ long long i8_rfl64(long long v)
+{
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)((unsigned long long)v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+// block of global tile t (t inside the launch's tiles)
+__device__ __forceinline__ int i8_blk_of(const LDS_AS i8_tab_lds *tab, int t)
+{
+    int b = 0;
+    const int nb = i8_rfl(tab->nblk);
+    for (int j = 1; j < nb; j++) b += t >= i8_rfl(tab->t0[j]) ? 1 : 0;
+    return b;
+}
+
 // ---------------------------------------------------------------------------
 // k_dist_topk_i8
 //
@@ -199,7 +235,7 @@ __global__ __launch_bounds__(256) void k_shadow8(signed char *__restrict__ dst, 
 template <int KL, int NKS, int W, int WPS, int NST, int NB>
 __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     const signed char *__restrict__ qsh, size_t q_rows_pad, size_t q_base, int nq,
-    const signed char *__restrict__ csh, size_t c_rows_pad, size_t c_base, int nc, int rs,
+    const knn_i8_blocks_t cb, size_t c_rows_pad, int rs,
     int nks, int ntiles, int nsplit, int nqb, double *__restrict__ part_d,
     int *__restrict__ part_i, double *__restrict__ part_T, int nq_pad,
     unsigned long long *__restrict__ qthr, int uj)
@@ -210,14 +246,17 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     constexpr int NORM0 = NST * 16384;
     constexpr int BUF0 = NORM0 + NST * 512; // [W][NB][64] survivor d^2, then ids
     constexpr int XB0 = BUF0 + 2 * W * NB * 256;   // W = 8: [8][32] bound exchange
-    constexpr int LDSB = XB0 + (W == 8 ? 8 * 32 * 4 : 0);
+    constexpr int TB0 = XB0 + (W == 8 ? 8 * 32 * 4 : 0);   // block table
+    constexpr int LDSB = TB0 + (int)((sizeof(i8_tab_lds) + 15) / 16 * 16);
     __shared__ __attribute__((aligned(16))) char smem[LDSB];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wave_s = __builtin_amdgcn_readfirstlane(wave);
     const int qg = wave_s & 3, rh = wave_s >> 2;
     const int r32 = lane & 31, h = lane >> 5;
+    // split-major order: long splits first (knn_engine.c: choose_splits);
+    // a query block's later splits start from the bounds its earlier ones
+    // published (qthr)
     const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;
-    // long splits first (split-major dispatch, knn_engine.c: choose_splits)
     const int tb = ntiles / nsplit, tr = ntiles - tb * nsplit;
     const int t_lo = split * tb + (split < tr ? split : tr);
     const int t_hi = t_lo + tb + (split < tr ? 1 : 0);
@@ -227,7 +266,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     constexpr int NCH = (NKS + 3) / 4;      // chunks a tile
     const int nch = NCH;
     const int *qnorms = (const int *)(qsh + q_rows_pad * (size_t)rs);
-    const int *cnorms = (const int *)(csh + c_rows_pad * (size_t)rs);
+    const size_t cnorm_off = c_rows_pad * (size_t)rs;   // norms behind the rows of every block
 
     // ---- resident query fragments (B), one per K-step --------------------
     // NKS >= nks K-steps (the instantiation's bucket): those past nks get
@@ -272,10 +311,22 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     LDS_AS int *bk = (LDS_AS int *)(smem + BUF0) + wave_s * NB * 64 + lane;   // entry e at bk[64 e]
     LDS_AS int *bi = bk + W * NB * 64;
     int cnt = 0;   // buffered survivors of this lane
+    LDS_AS i8_tab_lds *tab = (LDS_AS i8_tab_lds *)(smem + TB0);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int j = 0; j < KNN_I8_MAXBLK; j++) {
+            tab->ptr[j] = (unsigned long long)(uintptr_t)cb.ptr[j];
+            tab->base[j] = cb.base[j];
+            tab->nc[j] = cb.nc[j];
+        }
+#pragma unroll
+        for (int j = 0; j <= KNN_I8_MAXBLK; j++) tab->t0[j] = cb.t0[j];
+        tab->nblk = cb.nblk;
+    }
     if constexpr (W == 8) {
         if (h == 0) xb[wave_s * 32 + r32] = I8_INF;
-        __syncthreads();
     }
+    __syncthreads();
 
     // ---- staging ---------------------------------------------------------
     const int total = (t_hi > t_lo) ? (t_hi - t_lo) * nch : 0;
@@ -286,22 +337,33 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         voff[p] = (unsigned)(rr * rs + 16 * ((lane & 7) ^ ((rr >> 1) & 7)));
     }
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
+    // staging position: global tile s_t (block s_b, tile s_t - t0[s_b] of it),
+    // chunk s_c; wave-uniform, so the block lookups are scalar selects
     int s_t = t_lo, s_c = 0, s_x = 0;
+    int s_b = i8_blk_of(tab, t_lo);
+    const signed char *s_ptr = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]);
+    int s_t0 = i8_rfl(tab->t0[s_b]), s_t1 = i8_rfl(tab->t0[s_b + 1]);
     auto stage = [&]() {
-        const signed char *base = csh + (size_t)s_t * 128 * rs + 128 * s_c;
+        const size_t lt = (size_t)(s_t - s_t0);
+        const signed char *base = s_ptr + lt * 128 * rs + 128 * s_c;
         const unsigned dst = lds0 + (unsigned)(s_x % NST) * 16384u + (unsigned)wave_s * (16384u / W);
-        if constexpr (PW == 4) bglds16x4(knn_rsrc(base), voff[0], voff[1], voff[2], voff[3], dst);
-        else bglds16x2(knn_rsrc(base), voff[0], voff[1], dst);
+        if constexpr (PW == 4) bglds16x4(i8_rsrc(base), voff[0], voff[1], voff[2], voff[3], dst);
+        else bglds16x2(i8_rsrc(base), voff[0], voff[1], dst);
         if (s_x < total && s_c == 0) {
             if (lane < 32 / W)
-                bglds16(knn_rsrc(cnorms + (size_t)s_t * 128 + (128 / W) * wave_s), 16u * lane,
+                bglds16(i8_rsrc((const int *)(s_ptr + cnorm_off) + lt * 128 + (128 / W) * wave_s), 16u * lane,
                         lds0 + NORM0 + (unsigned)(s_t % NST) * 512u + (512u / W) * wave_s);
         }
         s_x++;
         if (s_x < total) {
             if (++s_c == nch) {
                 s_c = 0;
-                s_t++;
+                if (++s_t == s_t1) {   // next block of the launch
+                    s_b++;
+                    s_ptr = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]);
+                    s_t0 = s_t1;
+                    s_t1 = i8_rfl(tab->t0[s_b + 1]);
+                }
             }
         }
     };
@@ -364,7 +426,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     };
 
     // ---- epilogue of tile t --------------------------------------------------
+    // t: global tile of the launch; lt / c_base / nc: its block's tile,
+    // first global id and rows (kept by the main loop)
+    long c_base = 0;
+    int nc = 0, e_t0 = 0, e_t1 = 0, e_b = 0;
     auto epilogue = [&](int t, knn_v16i (&A)[MB]) {
+        const int lt = t - e_t0;
         const LDS_AS knn_v4i *cn =
             (const LDS_AS knn_v4i *)((LDS_AS char *)smem + NORM0 + (t % NST) * 512) + 4 * h + 8 * MB * rh;
         const int lim = L[KL - 1] < thr ? L[KL - 1] : thr;
@@ -383,7 +450,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 }
             }
         }
-        const int row0 = t * 128 + 32 * MB * rh;
+        const int row0 = lt * 128 + 32 * MB * rh;
         const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 32 * qg;
         const bool masked = (row0 + 32 * MB > nc) || (gw0 < gt0 + 32 * MB && gt0 < gw0 + 32);
         if (!masked && __ballot(lmn <= limq) == 0ull) return;   // common late in the scan
@@ -459,7 +526,19 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         rdA(0, 0, acur);
         stage();
         int x = 0;
+        e_b = i8_blk_of(tab, t_lo);
+        e_t0 = i8_rfl(tab->t0[e_b]);
+        e_t1 = i8_rfl(tab->t0[e_b + 1]);
+        c_base = (long)i8_rfl64(tab->base[e_b]);
+        nc = i8_rfl(tab->nc[e_b]);
         for (int t = t_lo; t < t_hi; t++) {
+            if (t == e_t1) {   // the epilogue's block moves on
+                e_b++;
+                e_t0 = e_t1;
+                e_t1 = i8_rfl(tab->t0[e_b + 1]);
+                c_base = (long)i8_rfl64(tab->base[e_b]);
+                nc = i8_rfl(tab->nc[e_b]);
+            }
             knn_v16i acc[MB];
 #pragma unroll
             for (int bb = 0; bb < MB; bb++)
@@ -551,34 +630,50 @@ extern "C" int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t 
 
 template <int KL, int NKS, int W, int WPS, int NST, int NB>
 static void launch_i8(dim3 grid, hipStream_t s, const void *qsh, size_t q_rows_pad, size_t q_base,
-                      int nq, const void *csh, size_t c_rows_pad, size_t c_base, int nc, int rs,
+                      int nq, const knn_i8_blocks_t &cb, size_t c_rows_pad, int rs,
                       int nks, int ntiles, int nsplit, int nqb, double *part_d, int *part_i,
                       double *part_T, int nq_pad, double *qthr, int uj)
 {
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KL, NKS, W, WPS, NST, NB>), grid, dim3(64 * W), 0, s,
-                       (const signed char *)qsh, q_rows_pad, q_base, nq, (const signed char *)csh,
-                       c_rows_pad, c_base, nc, rs, nks, ntiles, nsplit, nqb, part_d, part_i, part_T,
-                       nq_pad, (unsigned long long *)qthr, uj);
+                       (const signed char *)qsh, q_rows_pad, q_base, nq, cb, c_rows_pad, rs, nks, ntiles,
+                       nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj);
 }
 
 extern "C" int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_pad, size_t q_base,
-                                  int nq, const void *csh, size_t c_rows_pad, size_t c_base, int nc,
-                                  int n, int nsplit, double *part_d, int *part_i, double *part_T,
+                                  int nq, const knn_i8_blocks_t *cbp, size_t c_rows_pad, int n,
+                                  int nsplit, double *part_d, int *part_i, double *part_T,
                                   int nq_pad, double *qthr, void *stream)
 {
     const int rs = (int)knn_s8_rs((size_t)n), nks = rs / 32;
-    const int nqb = (nq + 127) / 128, ntiles = (nc + 127) / 128;
+    const int nqb = (nq + 127) / 128;
     const int kl = knn_i8_kl(kp);
+    if (!cbp || cbp->nblk < 1 || cbp->nblk > KNN_I8_MAXBLK) return KNN_ERR_INVALID;
+    // the table the kernel walks: block b = tiles [t0[b], t0[b+1]) of its
+    // ceil(nc/128) tiles, ascending bases, rows inside the capacity
+    knn_i8_blocks_t cb = *cbp;
+    cb.t0[0] = 0;
+    for (int b = 0; b < cb.nblk; b++) {
+        if (!cb.ptr[b] || cb.nc[b] <= 0 || (size_t)cb.nc[b] > c_rows_pad || cb.base[b] < 0 ||
+            (b > 0 && cb.base[b] < cb.base[b - 1] + cb.nc[b - 1]))
+            return KNN_ERR_INVALID;
+        cb.t0[b + 1] = cb.t0[b] + (cb.nc[b] + 127) / 128;
+    }
+    for (int b = cb.nblk; b < KNN_I8_MAXBLK; b++) {
+        cb.ptr[b] = cb.ptr[cb.nblk - 1];
+        cb.base[b] = cb.base[cb.nblk - 1];
+        cb.nc[b] = cb.nc[cb.nblk - 1];
+        cb.t0[b + 1] = cb.t0[cb.nblk];
+    }
+    const int ntiles = cb.t0[cb.nblk];
     if (nqb <= 0 || nsplit <= 0 || k <= 0 || k > kp || kl <= 0 || nks > 28) return KNN_ERR_INVALID;
-    if ((size_t)nqb * 128 > q_rows_pad || (size_t)ntiles * 128 > c_rows_pad || nq_pad < nqb * 128)
-        return KNN_ERR_INVALID;
+    if ((size_t)nqb * 128 > q_rows_pad || nq_pad < nqb * 128) return KNN_ERR_INVALID;
     // lane-list slot of the shared bound: the 2 lanes of a query cover k + 1
     int uj = (k + 1 + 1) / 2 - 1, uj4 = (k + 1 + 3) / 4 - 1;
     if (uj > kl - 1) uj = kl - 1;
     uj |= uj4 << 8;
     const dim3 grid((unsigned)(nqb * nsplit));
     hipStream_t s = (hipStream_t)stream;
-#define I8_ARGS grid, s, qsh, q_rows_pad, q_base, nq, csh, c_rows_pad, c_base, nc, rs, nks, ntiles, nsplit, \
+#define I8_ARGS grid, s, qsh, q_rows_pad, q_base, nq, cb, c_rows_pad, rs, nks, ntiles, nsplit, \
                 nqb, part_d, part_i, part_T, nq_pad, qthr, uj
     // One workgroup a CU (queries in up to 112 VGPRs), an 8-stage ring.
     // k <= 32: 8 waves (two a SIMD, 2 m-blocks each, 4 lists a query) and

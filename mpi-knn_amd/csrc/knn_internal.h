@@ -80,6 +80,18 @@ static inline size_t knn_s8_bytes(size_t cap, size_t n)
 {
     return knn_round_up(knn_s8_norm_offset(cap, n) + knn_rows_pad(cap) * 4 + 8 * sizeof(double), 16);
 }
+/* Corpus blocks of one k_dist_topk_i8 launch (a fused ring step): byte
+ * blocks of one capacity, ascending global base (so every lane meets its
+ * candidates in increasing row order: the stable tie rule), block b holding
+ * global tiles [t0[b], t0[b+1]) of the launch. */
+#define KNN_I8_MAXBLK 8
+typedef struct {
+    const void *ptr[KNN_I8_MAXBLK];
+    int64_t base[KNN_I8_MAXBLK];
+    int nc[KNN_I8_MAXBLK];
+    int t0[KNN_I8_MAXBLK + 1];
+    int nblk;
+} knn_i8_blocks_t;
 static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL : KNN_I8_KL_L; }
 static inline int knn_i8_lpq(int kp) { return kp <= KNN_KP_M ? 4 : 2; }
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
@@ -109,7 +121,7 @@ int knn_launch_fill_inf(double *p, int count, void *stream);
 int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,
                        const double *meta, void *stream);
 int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_pad, size_t q_base, int nq,
-                       const void *csh, size_t c_rows_pad, size_t c_base, int nc, int n, int nsplit,
+                       const knn_i8_blocks_t *cb, size_t c_rows_pad, int n, int nsplit,
                        double *part_d, int *part_i, double *part_T, int nq_pad, double *qthr,
                        void *stream);
 int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *part_i,

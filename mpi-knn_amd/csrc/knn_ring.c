@@ -16,10 +16,22 @@
  * results are byte-identical to the 1-GPU path (merge order is by (d, idx)).
  * The meta of all blocks is combined with one ncclAllReduce(max).
  *
+ * Two schedules (KNN_RING_SCHEDULE, default "direct"):
+ *   ring    the rotation above, one hop per step;
+ *   direct  every device sends its block to every other device at once (one
+ *           ncclGroup of P-1 sends and P-1 receives per device: on a fully
+ *           connected xGMI node each transfer has a link of its own) while it
+ *           folds its own block, then folds the P-1 received blocks -- int8
+ *           byte blocks in one fused launch (knn_ctx_step_shadow_n).
+ * Both move the search's shadow form when it has one (int8 byte blocks,
+ * fp16 rows: knn_ctx_shadow) and element blocks otherwise; the exact rescan
+ * always reads element blocks.
+ *
  * The hop is a transport: RCCL over the node's GPUs, or (KNN_RING_LOOPBACK=1)
- * a loopback of P virtual ranks on device 0 whose hop is P device copies on
- * one "fabric" stream -- the same schedule, buffers, events and lag rule,
- * so the P >= 2 ring is testable on a one-GPU box (tests/test_gpu_ring_rotation.py).
+ * a loopback of P virtual ranks on device 0 whose transfers are device
+ * copies on one "fabric" stream -- the same schedules, buffers, events and
+ * lag rule, so the P >= 2 ring is testable on a one-GPU box
+ * (tests/test_gpu_parity.py).
  */
 #include "knn_internal.h"
 
@@ -42,7 +54,9 @@ typedef struct {
     int dev;
     size_t rows, base;          /* own block */
     void *qb;                   /* own packed block: the queries, never overwritten */
-    void *rx[KNN_STEP_LAG + 2]; /* receive buffers (capacity R) */
+    void *qs;                   /* own block in the search's shadow form (or NULL) */
+    void **rx;                  /* nrx receive buffers (element-block capacity R):
+                                 * ring NRX, direct P - 1 (rx[j-1] <- block g - j) */
     void *cur, *nxt;            /* block being folded / being received */
     int hop;                    /* hops made: hop h lands in rx[h % NRX] */
     double *src;                /* raw rows of the own block */
@@ -103,10 +117,130 @@ static int ring_hop(ring_dev_t *d, int P, size_t bytes, ring_transport_t *t)
     return KNN_OK;
 }
 
+static size_t rows_of(int b, size_t R, size_t m)
+{
+    const size_t base = (size_t)b * R;
+    return (base + R <= m) ? R : m - base;
+}
+
+/* One step's fold of the block at `blk` (form: 0 element, else shadow) */
+static int fold_one(ring_dev_t *e, const void *blk, size_t rows, size_t base, int rescan, int form)
+{
+    if (rescan) return knn_ctx_rescan_step(e->ctx, blk, rows, base, e->cs);
+    return form ? knn_ctx_step_shadow(e->ctx, blk, rows, base, e->cs)
+                : knn_ctx_step(e->ctx, blk, rows, base, e->cs);
+}
+
+/* Direct exchange: device g's `send` block to every other device, rx[j-1]
+ * of device g receiving block g - j, all transfers of all devices in one
+ * group (RCCL) or on the fabric stream (loopback); ev_comm marks arrival. */
+static int direct_exchange(ring_dev_t *d, int P, size_t bytes, void *const *send, ring_transport_t *t)
+{
+    if (t->kind == RING_LOOPBACK) {
+        if (hipSetDevice(d[0].dev) != hipSuccess) return KNN_ERR_HIP;
+        for (int g = 0; g < P; g++)
+            if (hipStreamWaitEvent(t->fabric, d[g].ev_comp, 0) != hipSuccess) return KNN_ERR_HIP;
+        for (int g = 0; g < P; g++)
+            for (int j = 1; j < P; j++)
+                if (hipMemcpyAsync(d[g].rx[j - 1], send[(g - j + P) % P], bytes, hipMemcpyDeviceToDevice,
+                                   t->fabric) != hipSuccess)
+                    return KNN_ERR_HIP;
+        for (int g = 0; g < P; g++)
+            if (hipEventRecord(d[g].ev_comm, t->fabric) != hipSuccess) return KNN_ERR_HIP;
+        return KNN_OK;
+    }
+    for (int g = 0; g < P; g++) {
+        if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
+        if (hipStreamWaitEvent(d[g].ms, d[g].ev_comp, 0) != hipSuccess) return KNN_ERR_HIP;
+    }
+    if (ncclGroupStart() != ncclSuccess) return KNN_ERR_RCCL;
+    for (int g = 0; g < P; g++)
+        for (int j = 1; j < P; j++)
+            if (ncclSend(send[g], bytes, ncclUint8, (g + j) % P, d[g].comm, d[g].ms) != ncclSuccess ||
+                ncclRecv(d[g].rx[j - 1], bytes, ncclUint8, (g - j + P) % P, d[g].comm, d[g].ms) !=
+                    ncclSuccess) {
+                ncclGroupEnd();
+                return KNN_ERR_RCCL;
+            }
+    if (ncclGroupEnd() != ncclSuccess) return KNN_ERR_RCCL;
+    for (int g = 0; g < P; g++) {
+        if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
+        if (hipEventRecord(d[g].ev_comm, d[g].ms) != hipSuccess) return KNN_ERR_HIP;
+    }
+    return KNN_OK;
+}
+
+/* One direct pass: exchange (form: 0 element blocks, else the shadow form),
+ * every device folds its own block, then the P-1 received ones. */
+static int direct_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t n, int dtype, int rescan,
+                       int form, ring_transport_t *t)
+{
+    void *send[KNN_RING_MAX];
+    const void *blk[KNN_RING_MAX];
+    size_t nc[KNN_RING_MAX], base[KNN_RING_MAX];
+    int rc;
+    /* the own block is folded while the blocks travel, then the received
+     * ones in one fused launch; KNN_RING_FUSE=all folds all P byte blocks in
+     * one launch after the exchange */
+    const char *fz = getenv("KNN_RING_FUSE");
+    const int fuse_all = form && !rescan && P > 1 && knn_ctx_shadow(d[0].ctx) == 2 && fz &&
+                         strcmp(fz, "all") == 0;
+    const size_t bytes = form ? knn_ctx_shadow_bytes(d[0].ctx, R)
+                              : knn_block_bytes_dt(R, n, dtype);
+    for (int g = 0; g < P; g++) send[g] = form ? d[g].qs : d[g].qb;
+    if (P > 1 && (rc = direct_exchange(d, P, bytes, send, t))) return rc;
+    for (int g = 0; g < P && !fuse_all; g++) {
+        if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
+        if ((rc = fold_one(&d[g], send[g], d[g].rows, d[g].base, rescan, form))) return rc;
+    }
+    for (int g = 0; g < P && P > 1; g++) {
+        ring_dev_t *e = &d[g];
+        if (hipSetDevice(e->dev) != hipSuccess) return KNN_ERR_HIP;
+        if (hipStreamWaitEvent(e->cs, e->ev_comm, 0) != hipSuccess) return KNN_ERR_HIP;
+        for (int j = 1; j < P; j++) {
+            const int b = (g - j + P) % P;
+            blk[j] = e->rx[j - 1];
+            base[j] = (size_t)b * R;
+            nc[j] = rows_of(b, R, m);
+        }
+        blk[0] = send[g];
+        base[0] = e->base;
+        nc[0] = e->rows;
+        if (fuse_all) {
+            rc = knn_ctx_step_shadow_n(e->ctx, P, blk, nc, base, e->cs);
+        } else if (form && !rescan) {
+            rc = knn_ctx_step_shadow_n(e->ctx, P - 1, blk + 1, nc + 1, base + 1, e->cs);
+        } else {
+            rc = KNN_OK;
+            for (int j = 1; j < P && !rc; j++) rc = fold_one(e, blk[j], nc[j], base[j], rescan, form);
+        }
+        if (rc) return rc;
+        if (hipEventRecord(e->ev_comp, e->cs) != hipSuccess) return KNN_ERR_HIP;
+    }
+    return KNN_OK;
+}
+
+/* Rescan over the element blocks a direct pass left resident */
+static int direct_pass_resident(ring_dev_t *d, int P, size_t R, size_t m)
+{
+    int rc;
+    for (int g = 0; g < P; g++) {
+        ring_dev_t *e = &d[g];
+        if (hipSetDevice(e->dev) != hipSuccess) return KNN_ERR_HIP;
+        if ((rc = knn_ctx_rescan_step(e->ctx, e->qb, e->rows, e->base, e->cs))) return rc;
+        for (int j = 1; j < P; j++) {
+            const int b = (g - j + P) % P;
+            if ((rc = knn_ctx_rescan_step(e->ctx, e->rx[j - 1], rows_of(b, R, m), (size_t)b * R, e->cs)))
+                return rc;
+        }
+    }
+    return KNN_OK;
+}
+
 /* One full rotation: at step s device g folds block (g - off - s) mod P,
  * where off says how far the blocks have already moved. */
 static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int off,
-                     int rescan, ring_transport_t *t)
+                     int rescan, int form, ring_transport_t *t)
 {
     int rc;
     for (int s = 0; s < P; s++) {
@@ -114,10 +248,9 @@ static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int
         for (int g = 0; g < P; g++) {
             const int b = ((g - off - s) % P + P) % P;
             const size_t base = (size_t)b * R;
-            const size_t rows = (base + R <= m) ? R : m - base;
+            const size_t rows = rows_of(b, R, m);
             if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
-            rc = rescan ? knn_ctx_rescan_step(d[g].ctx, d[g].cur, rows, base, d[g].cs)
-                        : knn_ctx_step(d[g].ctx, d[g].cur, rows, base, d[g].cs);
+            rc = fold_one(&d[g], d[g].cur, rows, base, rescan, form);
             if (rc) return rc;
             if (hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) return KNN_ERR_HIP;
         }
@@ -167,6 +300,9 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
     const size_t bytes = knn_block_bytes_dt(R, n, dtype);
     if (bytes == 0) return KNN_ERR_INVALID;
 
+    const char *sch = getenv("KNN_RING_SCHEDULE");
+    const int direct = !(sch && strcmp(sch, "ring") == 0);
+    const int nrx = (direct && P - 1 > NRX) ? P - 1 : NRX;
     ring_dev_t d[KNN_RING_MAX];
     memset(d, 0, sizeof(d));
     int devs[KNN_RING_MAX];
@@ -196,8 +332,8 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             rc = KNN_ERR_HIP;
             break;
         }
-        int rx_ok = 1;
-        for (int b = 0; b < NRX; b++) rx_ok &= hipMalloc(&e->rx[b], bytes) == hipSuccess;
+        int rx_ok = (e->rx = (void **)calloc((size_t)nrx, sizeof(void *))) != NULL;
+        for (int b = 0; b < nrx && rx_ok; b++) rx_ok &= hipMalloc(&e->rx[b], bytes) == hipSuccess;
         if (!rx_ok || hipMalloc(&e->qb, bytes) != hipSuccess ||
             hipMalloc((void **)&e->src, e->rows * n * sizeof(double)) != hipSuccess ||
             hipMalloc((void **)&e->meta, KNN_META_DOUBLES * sizeof(double)) != hipSuccess ||
@@ -264,12 +400,26 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             if (hipMemcpyAsync(d[g].meta, hm, sizeof(hm), hipMemcpyHostToDevice, d[g].cs) != hipSuccess)
                 rc = KNN_ERR_HIP;
     }
+    /* the form blocks travel in: the search's shadow form when it has one
+     * (P > 1; KNN_NO_SHADOW_RING=1 keeps element blocks) */
+    const char *nsr = getenv("KNN_NO_SHADOW_RING");
+    int form = 0;
     for (int g = 0; g < P && !rc; g++) {
         hipSetDevice(d[g].dev);
         rc = knn_ctx_begin_meta(d[g].ctx, d[g].qb, R, d[g].base, d[g].meta, hm, d[g].cs);
+        if (!rc && g == 0) form = P > 1 && knn_ctx_shadow(d[g].ctx) != 0 && !(nsr && nsr[0] == '1');
+        if (!rc && form) {
+            if (!d[g].qs && hipMalloc(&d[g].qs, knn_ctx_shadow_bytes(d[g].ctx, R)) != hipSuccess)
+                rc = KNN_ERR_NOMEM;
+            if (!rc) rc = knn_ctx_shadow_pack(d[g].ctx, d[g].qs, d[g].qb, R, d[g].cs);
+            d[g].cur = d[g].qs;
+        }
         if (!rc && hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
     }
-    if (!rc) rc = ring_pass(d, P, R, m, bytes, 0, 0, &tr);
+    if (!rc && direct)
+        rc = direct_pass(d, P, R, m, n, dtype, 0, form, &tr);
+    else if (!rc)
+        rc = ring_pass(d, P, R, m, form ? knn_ctx_shadow_bytes(d[0].ctx, R) : bytes, 0, 0, form, &tr);
     size_t unresolved_total = 0;
     for (int g = 0; g < P && !rc; g++) {
         size_t u = 0;
@@ -285,7 +435,21 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             hipSetDevice(d[g].dev);
             if (hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
         }
-        if (!rc) rc = ring_pass(d, P, R, m, bytes, P - 1, 1, &tr);
+        if (!rc && direct) {
+            /* element blocks: exchanged again after a shadow-form pass (the
+             * receive buffers held shadow blocks), else still resident */
+            rc = form ? direct_pass(d, P, R, m, n, dtype, 1, 0, &tr)
+                      : direct_pass_resident(d, P, R, m);
+        } else if (!rc && form) {
+            /* the pass moved shadow blocks: a fresh rotation of element blocks */
+            for (int g = 0; g < P; g++) {
+                d[g].cur = d[g].qb;
+                d[g].nxt = d[g].rx[++d[g].hop % NRX];
+            }
+            rc = ring_pass(d, P, R, m, bytes, 0, 1, 0, &tr);
+        } else if (!rc) {
+            rc = ring_pass(d, P, R, m, bytes, P - 1, 1, 0, &tr);
+        }
         for (int g = 0; g < P && !rc; g++) {
             hipSetDevice(d[g].dev);
             rc = knn_ctx_rescan_end(d[g].ctx, d[g].d_out, d[g].cs);
@@ -311,7 +475,9 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         hipSetDevice(d[g].dev);
         if (d[g].ctx) knn_ctx_destroy(d[g].ctx);
         hipFree(d[g].qb);
-        for (int b = 0; b < NRX; b++) hipFree(d[g].rx[b]);
+        hipFree(d[g].qs);
+        for (int b = 0; b < nrx && d[g].rx; b++) hipFree(d[g].rx[b]);
+        free(d[g].rx);
         hipFree(d[g].src);
         hipFree(d[g].meta);
         hipFree(d[g].d_out);

@@ -45,7 +45,7 @@ API_SYMBOLS = (
     "knn_ctx_contraction_bits", "knn_wire_bytes", "knn_wire_ok", "knn_wire_pack",
     "knn_wire_unpack", "knn_shadow_bytes", "knn_shadow_norm_offset", "knn_shadow_pack",
     "knn_ctx_shadow", "knn_ctx_step_shadow", "knn_ctx_begin_meta", "knn_ctx_shadow_bytes",
-    "knn_ctx_shadow_pack",
+    "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -116,6 +116,7 @@ def _load():
         "knn_shadow_pack": ([p, p, sz, sz, i, p], i),
         "knn_ctx_shadow": ([p], i),
         "knn_ctx_step_shadow": ([p, p, sz, sz, p], i),
+        "knn_ctx_step_shadow_n": ([p, i, pp, psz, psz, p], i),
         "knn_ctx_profile": ([p, i, ctypes.POINTER(d), ctypes.POINTER(d), ctypes.POINTER(i)], i),
     }
     for name, (args, res) in sig.items():
@@ -323,6 +324,16 @@ class Context:
     def step_shadow(self, d_sblock, nc, c_base, stream=0):
         _check(lib.knn_ctx_step_shadow(self._h, d_sblock, nc, c_base, stream or None),
                "knn_ctx_step_shadow")
+
+    def step_shadow_n(self, d_sblocks, ncs, c_bases, stream=0):
+        """several resident shadow-form blocks in one step (int8 byte
+        blocks: one fused distance launch per 8 blocks)"""
+        nb = len(d_sblocks)
+        ptrs = (ctypes.c_void_p * nb)(*d_sblocks)
+        ncv = (ctypes.c_size_t * nb)(*ncs)
+        cbv = (ctypes.c_size_t * nb)(*c_bases)
+        _check(lib.knn_ctx_step_shadow_n(self._h, nb, ptrs, ncv, cbv, stream or None),
+               "knn_ctx_step_shadow_n")
 
     def shadow(self):
         """Shadow form of this search (after begin): 0 none, 1 fp16 shadow

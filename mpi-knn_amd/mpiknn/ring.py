@@ -88,13 +88,23 @@ class GpuEngine:
         self.meta.copy_(self.qb[self.meta_off:self.meta_off + 8 * self.mk.META_DOUBLES]
                         .view(self.torch.float64))
 
-    def wires(self):
-        """own wire block + two wire receive buffers (allocated on first use)"""
-        if self._wires is None:
+    def wires(self, count=3):
+        """own wire block + wire receive buffers (at least `count` in all,
+        allocated on first use)"""
+        if self._wires is None or len(self._wires) < count:
             wb = self.mk.wire_bytes(self.R, self.n, self.dtype)
             self._wires = tuple(self.torch.empty(wb, dtype=self.torch.uint8, device=self.dev)
-                                for _ in range(3))
+                                for _ in range(max(3, count)))
         return self._wires
+
+    def recv_buffers(self, count):
+        """`count` element-block receive buffers (the direct exchange keeps
+        every other rank's block resident: P - 1 of them)"""
+        if len(self.rx) < count:
+            nb = self.mk.block_bytes(self.R, self.n, self.dtype)
+            self.rx = self.rx + tuple(self.torch.empty(nb, dtype=self.torch.uint8, device=self.dev)
+                                      for _ in range(count - len(self.rx)))
+        return self.rx[:count]
 
     def wire_pack(self, wire):
         self.mk.wire_pack(wire.data_ptr(), self.qb.data_ptr(), self.R, self.n, self.dtype,
@@ -123,6 +133,9 @@ class GpuEngine:
     def step_shadow(self, sbuf, rows, base):
         self.ctx.step_shadow(sbuf.data_ptr(), rows, base, self.stream())
 
+    def step_shadow_n(self, sbufs, rows, bases):
+        self.ctx.step_shadow_n([b.data_ptr() for b in sbufs], rows, bases, self.stream())
+
     def step(self, buf, rows, base, rescan=False):
         if rescan:
             self.ctx.rescan_step(buf.data_ptr(), rows, base, self.stream())
@@ -140,12 +153,28 @@ class GpuEngine:
         return host.view(self.mk.NB_DTYPE).reshape(-1, self.k)[: self.nq]
 
 
-def ring_search(dist, torch, engine, rank, P, m, q_base):
+def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
     """Run the ring on this rank.  `engine` holds the packed own block
-    (engine.pack done).  Collective calls: all_reduce(meta), P-1 hops per
-    pass, all_reduce(unresolved).  Returns the number of queries that took
-    the exact rescan pass on this rank."""
+    (engine.pack done).  Collective calls: all_reduce(meta), the block
+    exchange of each pass, all_reduce(unresolved).  Returns the number of
+    queries that took the exact rescan pass on this rank.
+
+    schedule (default: KNN_RING_SCHEDULE, else "direct"):
+      "ring"    P-1 hops to the right neighbour, one block folded per hop
+                (the reference's rotation, blk:187-244 / nb:196-259);
+      "direct"  every rank sends its block to every other rank at once --
+                P-1 point-to-point transfers, each on the xGMI link joining
+                the two GPUs of a fully connected node -- while the own block
+                is folded; the P-1 received blocks are then folded together
+                (one fused int8 launch for byte blocks, knn_ctx_step_shadow_n).
+                A ring hop carries one block over one link per step; the
+                direct exchange spreads the same bytes over all seven links of
+                an 8-GPU node in the time of one hop."""
     import os
+    if schedule is None:
+        schedule = os.environ.get("KNN_RING_SCHEDULE", "direct")
+    if schedule not in ("ring", "direct"):
+        raise ValueError("unknown ring schedule %r" % (schedule,))
     R, blocks = partition(m, P)
     wire = False
     h_meta = None
@@ -167,7 +196,8 @@ def ring_search(dist, torch, engine, rank, P, m, q_base):
         srx = tuple(b[:sb] for b in rx)      # shadow blocks fit the element buffers
         state["cur"] = state["send"] = own_s
     if wire:
-        own_w, wa, wb = engine.wires()
+        ws = engine.wires(P if schedule == "direct" else 3)
+        own_w, wa, wb = ws[0], ws[1], ws[2]
     if wire and not shadow:
         engine.wire_pack(own_w)
         state["send"] = own_w
@@ -199,14 +229,85 @@ def ring_search(dist, torch, engine, rank, P, m, q_base):
                 state["send"] = land
                 state["hop"] += 1
 
-    one_pass(0, False)
+    def recv_bufs(count):
+        if hasattr(engine, "recv_buffers"):
+            return engine.recv_buffers(count)
+        return tuple(torch.empty_like(engine.rx[0]) for _ in range(count))
+
+    def direct_pass(rescan, resident):
+        """own block first, then the P-1 others, received all at once.
+        resident: element blocks already held from the first pass (rescan)"""
+        use_shadow = shadow and not rescan
+        use_wire = wire and not use_shadow
+        own = own_s if use_shadow else engine.qb
+        peers = [(rank - j) % P for j in range(1, P)]   # buffer j-1 holds block rank - j
+        reqs, land, ebufs = [], [], []
+        if resident is None and P > 1:
+            ebufs = recv_bufs(P - 1)
+            if use_shadow:
+                land = [b[:sb] for b in ebufs]
+            elif use_wire:
+                land = list(engine.wires(P)[1:P])
+            else:
+                land = list(ebufs)
+            send = own_w if use_wire else own
+            if use_wire and rescan:   # the first pass moved shadow blocks
+                engine.wire_pack(own_w)
+            ops = []
+            for j in range(1, P):
+                ops.append(dist.P2POp(dist.isend, send, (rank + j) % P))
+                ops.append(dist.P2POp(dist.irecv, land[j - 1], (rank - j) % P))
+            reqs = dist.batch_isend_irecv(ops)
+        base, rows = blocks[rank]
+        # the own block is folded while the other blocks travel, then the
+        # received ones in one fused launch ("rest"); KNN_RING_FUSE=all waits
+        # for the exchange and folds all P blocks in one launch (the same
+        # compute time in the P = 4 / 8 emulation, the exchange exposed)
+        fuse = os.environ.get("KNN_RING_FUSE", "rest")
+        fuse_all = (use_shadow and fuse == "all" and P > 1 and resident is None and
+                    engine.ctx.shadow() == 2)
+        if fuse_all:
+            pass
+        elif use_shadow:
+            engine.step_shadow(own, rows, base)
+        else:
+            engine.step(own, rows, base, rescan)
+        for r in reqs:
+            r.wait()
+        if resident is not None:
+            fold = resident
+        elif use_wire:
+            fold = list(ebufs)
+            for j in range(P - 1):
+                engine.wire_unpack(fold[j], land[j])
+        else:
+            fold = land
+        bs = [blocks[b] for b in peers]
+        if fuse_all:
+            engine.step_shadow_n([own] + list(fold), [rows] + [r for _, r in bs],
+                                 [base] + [b for b, _ in bs])
+        elif use_shadow and len(fold) > 0:
+            engine.step_shadow_n(fold, [r for _, r in bs], [b for b, _ in bs])
+        else:
+            for buf, (b, r) in zip(fold, bs):
+                engine.step(buf, r, b, rescan)
+        return None if use_shadow else fold
+
+    if schedule == "direct":
+        held = direct_pass(False, None)
+    else:
+        one_pass(0, False)
     unresolved = engine.end()
     total = unresolved
     if P > 1:
         t = torch.tensor([float(unresolved)], dtype=torch.float64, device=engine.meta.device)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         total = int(t.item())
-    if total > 0:
+    if total > 0 and schedule == "direct":
+        # element blocks still resident unless the pass moved shadow blocks
+        direct_pass(True, held)
+        engine.rescan_end()
+    elif total > 0:
         if shadow:
             # the rescan needs element rows: a fresh rotation from the own block
             state.update(cur=engine.qb, send=engine.qb)

@@ -160,15 +160,25 @@ def test_ring_blocks_match_single_device(knn, oracle):
                 assert_same(got, oracle.knn(X, 30, rows=(base, rows)), "ring P=%d rank %d" % (P, g))
 
 
-@pytest.mark.parametrize("P", [2, 3, 4, 8])
+@pytest.mark.parametrize("schedule", ["ring", "direct", "direct-all", "ring-element"])
+@pytest.mark.parametrize("P", [2, 3, 4, 8, 11])
 @pytest.mark.parametrize("force_rescan", [False, True])
-def test_ring_driver_loopback(knn, oracle, monkeypatch, P, force_rescan):
-    """knn_ring.c's P >= 2 schedule (ring_pass / ring_hop, the receive-buffer
-    rotation, the off = P-1 rescan rotation) with its loopback transport: P
-    virtual ranks on device 0, each hop P device copies on one fabric
-    stream.  KNN_FORCE_RESCAN=1 sends every query through the exact rescan
-    pass, so that rotation is checked too.  Against the oracle."""
+def test_ring_driver_loopback(knn, oracle, monkeypatch, P, force_rescan, schedule):
+    """knn_ring.c's P >= 2 schedules with its loopback transport: P virtual
+    ranks on device 0, every transfer a device copy on one fabric stream.
+    "ring": ring_pass / ring_hop, the receive-buffer rotation and the rescan
+    rotation; "direct": the all-at-once exchange and the fused fold of the
+    received byte blocks (P = 11: launches of 8 + 2; "direct-all" with the
+    own block in the fused launch); these move the search's shadow form,
+    "ring-element" element blocks.  KNN_FORCE_RESCAN=1 sends
+    every query through the exact rescan pass, so its element-block pass is
+    checked too.  Against the oracle."""
     monkeypatch.setenv("KNN_RING_LOOPBACK", "1")
+    monkeypatch.setenv("KNN_RING_SCHEDULE", "ring" if schedule.startswith("ring") else "direct")
+    if schedule == "direct-all":
+        monkeypatch.setenv("KNN_RING_FUSE", "all")
+    if schedule == "ring-element":
+        monkeypatch.setenv("KNN_NO_SHADOW_RING", "1")
     if force_rescan:
         monkeypatch.setenv("KNN_FORCE_RESCAN", "1")
     for X in (datasets.mnist_like(1500, 784, seed=4)[0], datasets.digits_real()[0]):

@@ -9,8 +9,10 @@ stream lags KNN_STEP_LAG steps) are exercised with buffer reuse, and every rank'
 result must equal the oracle's serial scan of its rows (oracle.knn(X, k,
 rows=(base, rows)), serial:72-93) byte for byte -- in each hop form: element
 blocks, int16 wire blocks and the search's shadow form (int8 byte blocks on
-8-bit data, fp16 shadow rows on wider integers).  This replaces blk:187-244 /
-nb:196-259 with every block visited once.
+8-bit data, fp16 shadow rows on wider integers) -- and in both schedules
+(neighbour hops, and the direct exchange whose received byte blocks are
+folded by one fused launch).  This replaces blk:187-244 / nb:196-259 with
+every block visited once.
 """
 import types
 
@@ -27,7 +29,7 @@ class _Req:
         pass
 
 
-def loopback_dist(torch, rank, P, packed, metas, wires, engine):
+def loopback_dist(torch, rank, P, packed, metas, wires, engine, schedule="ring"):
     """A torch.distributed stand-in for rank `rank` of a P-ring whose packed
     blocks are `packed` (block b = rank b's own block), with wire forms
     (mpiknn.wire_pack) `wires`; shadow forms are made on first use with the
@@ -62,8 +64,9 @@ def loopback_dist(torch, rank, P, packed, metas, wires, engine):
     def batch_isend_irecv(ops):
         for fn, buf, peer in ops:
             if fn is irecv:
-                # hop h brings the block that started on rank - h - 1
-                b = (rank - hop["n"] - 1) % P
+                # ring: hop h brings the block that started on rank - h - 1;
+                # direct: the receive from a peer brings the peer's own block
+                b = peer if schedule == "direct" else (rank - hop["n"] - 1) % P
                 forms = {t[b].numel(): t[b] for t in (packed, wires)}
                 if engine.ctx.shadow():
                     sb = shadow(b)
@@ -78,10 +81,11 @@ def loopback_dist(torch, rank, P, packed, metas, wires, engine):
     return ns
 
 
+@pytest.mark.parametrize("schedule", ["ring", "direct"])
 @pytest.mark.parametrize("P", [2, 4, 7, 8])
 @pytest.mark.parametrize("kind", ["int", "real", "int-nowire", "int-noshadow", "int-fp16",
                                   "wide-int"])
-def test_ring_search_rotation(knn, oracle, P, kind, monkeypatch):
+def test_ring_search_rotation(knn, oracle, P, kind, schedule, monkeypatch):
     import torch
     import mpiknn.ring as ring
 
@@ -118,8 +122,8 @@ def test_ring_search_rotation(knn, oracle, P, kind, monkeypatch):
         wires.append(w)
     for g, e in enumerate(engines):
         base, rows = blocks[g]
-        d = loopback_dist(torch, g, P, packed, metas, wires, e)
-        ring.ring_search(d, torch, e, g, P, m, base)
+        d = loopback_dist(torch, g, P, packed, metas, wires, e, schedule)
+        ring.ring_search(d, torch, e, g, P, m, base, schedule=schedule)
         got = e.result()
         ref = oracle.knn(X, 30, rows=(base, rows))
         assert np.array_equal(got["idx"], ref["idx"]), (P, g)
@@ -149,9 +153,10 @@ def test_wire_round_trip(knn, dtype):
     assert not knn.wire_ok(np.array([32768.0, 0, 0, 0, 0, 0, 0, 0]))
 
 
+@pytest.mark.parametrize("schedule", ["ring", "direct"])
 @pytest.mark.parametrize("P", [2, 8])
 @pytest.mark.parametrize("shape", ["gist", "sift"])
-def test_ring_search_fp32_configs(knn, oracle, P, shape):
+def test_ring_search_fp32_configs(knn, oracle, P, shape, schedule):
     """configs[4] / configs[3] shapes through the real ring_search at reduced
     m: gist-like (real-valued fp32, n = 960, k = 100: fp32 GEMM filter +
     exact re-rank, element blocks on the link) and sift-like (integer fp32,
@@ -180,10 +185,54 @@ def test_ring_search_fp32_configs(knn, oracle, P, shape):
     metas = torch.stack([e.meta for e in engines])
     for g, e in enumerate(engines):
         base, rows = blocks[g]
-        d = loopback_dist(torch, g, P, packed, metas, packed, e)
-        ring.ring_search(d, torch, e, g, P, m, base)
+        d = loopback_dist(torch, g, P, packed, metas, packed, e, schedule)
+        ring.ring_search(d, torch, e, g, P, m, base, schedule=schedule)
         got = e.result()
         ref = oracle.knn(Xr, k, rows=(base, rows))
         assert np.array_equal(got["idx"], ref["idx"]), (shape, P, g)
         assert np.array_equal(got["distance"].view(np.uint64),
                               ref["distance"].view(np.uint64)), (shape, P, g)
+
+
+@pytest.mark.parametrize("fuse", ["rest", "all"])
+@pytest.mark.parametrize("P", [3, 12])
+def test_direct_fused_many_blocks(knn, oracle, P, fuse, monkeypatch):
+    """The direct schedule's fused step over more blocks than one launch
+    takes (P = 12: 11 or 12 byte blocks = launches of 8 + 3 / 8 + 4; "all"
+    folds the own block in the fused step too), with a forced rescan pass
+    over element blocks afterwards; every rank equals the oracle's scan of
+    its rows."""
+    import torch
+    import mpiknn.ring as ring
+    monkeypatch.setenv("KNN_FORCE_RESCAN", "1")
+    monkeypatch.setenv("KNN_RING_FUSE", fuse)
+    X = datasets.mnist_like(2400, 200, seed=11)[0]
+    X[1000] = X[17]                                   # a duplicate across blocks
+    m, n = X.shape
+    dev = torch.device("cuda", 0)
+    Xd = torch.from_numpy(X).to(dev)
+    R, blocks = ring.partition(m, P)
+    engines = []
+    for g in range(P):
+        base, rows = blocks[g]
+        e = ring.GpuEngine(torch, 0, n, R, rows, 30)
+        e.pack(Xd[base:base + rows], layout_col=False)
+        engines.append(e)
+    packed = [e.qb.clone() for e in engines]
+    metas = torch.stack([e.meta for e in engines])
+    wires = []
+    for e in engines:
+        w = torch.empty(knn.wire_bytes(R, n), dtype=torch.uint8, device=dev)
+        knn.wire_pack(w.data_ptr(), e.qb.data_ptr(), R, n, "f64", e.stream())
+        wires.append(w)
+    for g in (0, P // 2, P - 1):
+        e = engines[g]
+        base, rows = blocks[g]
+        d = loopback_dist(torch, g, P, packed, metas, wires, e, "direct")
+        ring.ring_search(d, torch, e, g, P, m, base, schedule="direct")
+        assert e.ctx.shadow() == 2
+        got = e.result()
+        ref = oracle.knn(X, 30, rows=(base, rows))
+        assert np.array_equal(got["idx"], ref["idx"]), (P, g)
+        assert np.array_equal(got["distance"].view(np.uint64),
+                              ref["distance"].view(np.uint64)), (P, g)

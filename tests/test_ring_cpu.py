@@ -1,8 +1,9 @@
 """The per-rank ring driver (mpiknn/ring.py) under gloo on CPU.
 
-world_size 2 and 3 processes run the real ring_search() schedule -- meta
-all-reduce, P-1 isend/irecv hops per pass with the query block kept
-resident, the rescan pass -- with a CPU stand-in engine whose per-block fold
+world_size 2, 3 and 4 processes run the real ring_search() schedules -- meta
+all-reduce, then either P-1 isend/irecv hops per pass with the query block
+kept resident ("ring") or one exchange of every block with every rank
+("direct"), and the rescan pass -- with a CPU stand-in engine whose per-block fold
 is the oracle's block restatement (test-only; the product engine is HIP).
 Every rank must end with exactly the serial-semantics lists of its rows and
 must have folded every block exactly once per pass.
@@ -92,8 +93,10 @@ def _worker(rank, world, port, force_rescan, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,force_rescan", [(2, False), (3, True)])
-def test_ring_schedule_gloo(world, force_rescan):
+@pytest.mark.parametrize("schedule", ["ring", "direct"])
+@pytest.mark.parametrize("world,force_rescan", [(2, False), (3, True), (4, True)])
+def test_ring_schedule_gloo(world, force_rescan, schedule, monkeypatch):
+    monkeypatch.setenv("KNN_RING_SCHEDULE", schedule)   # inherited by the spawned ranks
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -9,7 +9,8 @@
 #   trace:WL              rocprofv3 --kernel-trace --stats of a bench run
 #   pmc:WL:REP            FETCH_SIZE, WRITE_SIZE, MFMA-busy passes (REP
 #                         repetitions of each, one counter group per run)
-#   emu:WL[:RANKS[:STEPS]] tools/ring_emulate.py (per-rank ring work)
+#   emu:WL[:RANKS[:STEPS[:FUSE[:SPLITS]]]] tools/ring_emulate.py (per-rank ring
+#                         work; FUSE none|rest|all; SPLITS a comma list to sweep)
 #   emutrace:WL:RANKS     the same under --kernel-trace
 #   kb8:ARGS              tools/probe/kbench8.py ARGS (commas kept, '+' = space)
 set -o pipefail
@@ -55,11 +56,15 @@ run_step() {
       done
     done ;;
   emu)
-    local es
+    local es fz sw
     es=$(echo "$spec" | cut -s -d: -f4)
+    fz=$(echo "$spec" | cut -s -d: -f5)
+    sw=$(echo "$spec" | cut -s -d: -f6)
+    local lg="emu_${a}_${fz:-rest}_${b//,/-}${sw:+_sweep}.log"
     timeout -k 10 400 python -u tools/ring_emulate.py --workload "$a" --ranks "${b:-1,2,4,8}" --steps "${es:-5}" \
-      > "gpurun_out/emu_$a.log" 2>&1 || { rc=$?; tail -20 "gpurun_out/emu_$a.log"; fail "$spec" $rc; }
-    grep '"P"' "gpurun_out/emu_$a.log" ;;
+      ${fz:+--fuse $fz} ${sw:+--splits $sw} > "gpurun_out/$lg" 2>&1 \
+      || { rc=$?; tail -20 "gpurun_out/$lg"; fail "$spec" $rc; }
+    grep '"P"' "gpurun_out/$lg" ;;
   emutrace)
     (cd /tmp && export TMPDIR=/tmp && cd "$ROOT" &&
      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/emutrace_$a" -o run -- \

@@ -5,6 +5,7 @@
 // from the previous launch (converged), or taken as given (preset by the
 // driver).  Driven by tools/probe/kbench8.py (data from the real engine).
 #include "../../mpi-knn_amd/csrc/knn_i8.hip"
+#include <string.h>
 
 __global__ void kb8_fill_inf(double *p, int n)
 {
@@ -20,10 +21,18 @@ static void kb8_go(dim3 grid, const void *qsh, size_t q_rows_pad, int nq, const 
                    int nc, int rs, int nks, int ntiles, int nsplit, int nqb, double *part_d, int *part_i,
                    double *part_T, int nq_pad, double *qthr, int uj)
 {
+    knn_i8_blocks_t cb;   // one block: the whole corpus
+    memset(&cb, 0, sizeof(cb));
+    cb.nblk = 1;
+    for (int b = 0; b < KNN_I8_MAXBLK; b++) {
+        cb.ptr[b] = csh;
+        cb.nc[b] = nc;
+        cb.t0[b + 1] = ntiles;
+    }
+    cb.t0[0] = 0;
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KNN_I8_KL, NKS, 8, 2, NST, NB>), grid, dim3(512), 0, 0,
-                       (const signed char *)qsh, q_rows_pad, (size_t)0, nq, (const signed char *)csh, c_rows_pad,
-                       (size_t)0, nc, rs, nks, ntiles, nsplit, nqb, part_d, part_i, part_T, nq_pad,
-                       (unsigned long long *)qthr, uj);
+                       (const signed char *)qsh, q_rows_pad, (size_t)0, nq, cb, c_rows_pad, rs, nks, ntiles,
+                       nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj);
 }
 
 // average kernel ms over iters launches (after one warm-up); reset: 1 bounds

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--keep-qthr", action="store_true",
                     help="timed launches start from the previous launch's bounds (converged)")
     ap.add_argument("--m", type=int, default=0, help="use the first M rows (queries = corpus)")
+    ap.add_argument("--nq", type=int, default=0,
+                    help="queries = the first NQ rows (a P-way ring rank's fused launch: NQ = M / P)")
     ap.add_argument("--ideal-qthr", action="store_true",
                     help="bounds preset to each query's (k+1)-th d^2 over the FULL set (a late ring step)")
     a = ap.parse_args()
@@ -56,8 +58,9 @@ def main():
     sb = torch.empty(eng.ctx.shadow_bytes(m), dtype=torch.uint8, device="cuda:0")
     eng.ctx.shadow_pack(sb.data_ptr(), eng.qb.data_ptr(), m, eng.stream())
     torch.cuda.synchronize()
-    nq_pad = (m + 127) // 128 * 128
-    rp = nq_pad
+    nq = a.nq or m
+    nq_pad = (nq + 127) // 128 * 128
+    rp = (m + 127) // 128 * 128
     kl = 17   # KNN_I8_KL, 4 lists a query
     smax = max(int(x) for x in (a.splits or str(splits)).split(","))
     pd = torch.empty(smax * nq_pad * 4 * kl, dtype=torch.float64, device="cuda:0")
@@ -68,11 +71,11 @@ def main():
         # (k+1)-th nonzero d^2 of each query over all rows (exact: integer
         # data, fp64 sums far below 2^53)
         F = torch.from_numpy(np.ascontiguousarray(Xfull)).to("cuda:0").double()
-        Q = F[:m]
+        Q = F[:nq]
         nrm = (F * F).sum(1)
         b = torch.full((nq_pad,), float("inf"), dtype=torch.float64, device="cuda:0")
-        for lo in range(0, m, 1024):
-            hi = min(m, lo + 1024)
+        for lo in range(0, nq, 1024):
+            hi = min(nq, lo + 1024)
             d2 = nrm[lo:hi, None] + nrm[None, :] - 2.0 * Q[lo:hi] @ F.t()
             d2[d2 <= 0] = float("inf")
             b[lo:hi] = torch.topk(d2, k + 1, dim=1, largest=False).values[:, k]
@@ -81,13 +84,13 @@ def main():
     p, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     L.kbench8.argtypes = [i, p, sz, i, p, sz, i, i, i, i, p, p, p, i, p, i, i]
     L.kbench8.restype = ctypes.c_float
-    flop = 2.0 * m * m * n
+    flop = 2.0 * nq * m * n
     for var, splits in [(int(x), int(s)) for x in a.variant.split(",")
                         for s in (str(a.splits) if a.splits else str(splits)).split(",")]:
-        ms = L.kbench8(var, sb.data_ptr(), rp, m, sb.data_ptr(), rp, m, n, k, splits,
+        ms = L.kbench8(var, sb.data_ptr(), rp, nq, sb.data_ptr(), rp, m, n, k, splits,
                        pd.data_ptr(), pi.data_ptr(), pT.data_ptr(), nq_pad, qthr.data_ptr(), a.iters,
                        2 if a.ideal_qthr else (0 if a.keep_qthr else 1))
-        rec = {"workload": a.workload, "m": m, "keep_qthr": a.keep_qthr, "ideal": a.ideal_qthr,
+        rec = {"workload": a.workload, "m": m, "nq": nq, "keep_qthr": a.keep_qthr, "ideal": a.ideal_qthr,
                "variant": var, "splits": splits, "ms": ms,
                "tops": flop / (ms * 1e-3) / 1e12 if ms > 0 else None}
         if os.environ.get("KB8_TIMES"):

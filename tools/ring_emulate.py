@@ -64,6 +64,12 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--splits", default=None,
+                    help="comma list: repeat each P with KNN_SPLITS forced to each value (a sweep)")
+    ap.add_argument("--fuse", choices=("none", "rest", "all"), default="rest",
+                    help="byte-block steps: one launch per block (the neighbour ring), the own "
+                         "block then every other block in one launch (the direct-exchange "
+                         "ring's default), or all blocks in one launch (KNN_RING_FUSE=all)")
     args = ap.parse_args()
 
     import torch
@@ -75,7 +81,12 @@ def main():
     m = args.m or m0
     Xd = corpus(torch, args.workload, m, n, dev)
     res = {}
-    for P in [int(p) for p in args.ranks.split(",")]:
+    runs = [(int(p), None) for p in args.ranks.split(",")]
+    if args.splits:
+        runs = [(P, int(sp)) for P, _ in runs for sp in args.splits.split(",")]
+    for P, sp in runs:
+        if sp is not None:
+            os.environ["KNN_SPLITS"] = str(sp)
         R, blocks = ring.partition(m, P)
         eng = ring.GpuEngine(torch, 0, n, R, blocks[0][1], k, dtype=dt)
         sdt = "f32" if Xd.dtype == torch.float32 else "f64"
@@ -104,13 +115,23 @@ def main():
             eng.step(bufs[b], rows, base)
         eng.end()
 
+        fuse = args.fuse if shadow and eng.ctx.shadow() == 2 else "none"
+
         def one():
             eng.begin(0, h_meta=h_meta)
-            for b, (base, rows) in enumerate(blocks):
-                if shadow:
-                    eng.step_shadow(sbufs[b], rows, base)
-                else:
-                    eng.step(bufs[b], rows, base)
+            if fuse == "all":
+                eng.ctx.step_shadow_n([b.data_ptr() for b in sbufs], [r for _, r in blocks],
+                                      [bs for bs, _ in blocks], eng.stream())
+            elif fuse == "rest":
+                eng.step_shadow(sbufs[0], blocks[0][1], blocks[0][0])
+                eng.ctx.step_shadow_n([b.data_ptr() for b in sbufs[1:]], [r for _, r in blocks[1:]],
+                                      [bs for bs, _ in blocks[1:]], eng.stream())
+            else:
+                for b, (base, rows) in enumerate(blocks):
+                    if shadow:
+                        eng.step_shadow(sbufs[b], rows, base)
+                    else:
+                        eng.step(bufs[b], rows, base)
             return eng.end()
 
         one()
@@ -127,11 +148,16 @@ def main():
         res[P] = {"rank_ms": dt_s * 1e3, "dist_busy_ms_per_pass": dist_ms / args.steps,
                   "dist_tflops": flops / (dist_ms * 1e-3) / 1e12 if dist_ms > 0 else None,
                   "exposed_merge_ms_per_pass": merge_ms / args.steps,
-                  "splits": eng.ctx.info()[1], "shadow_ring": shadow,
+                  "splits": eng.ctx.info()[1], "shadow_ring": shadow, "fuse": fuse,
                   "contraction_bits": eng.ctx.contraction_bits(), "unresolved": unres}
         print(json.dumps({"P": P, **res[P]}), file=sys.stderr, flush=True)
+        if sp is not None:
+            res["%d/s%d" % (P, sp)] = res.pop(P)
         del bufs, sbufs, eng
         torch.cuda.empty_cache()
+    if args.splits:
+        print(json.dumps({"workload": args.workload, "sweep": res}, indent=1))
+        return
     t1 = res[min(res)]["rank_ms"] * min(res)
     for P, r in res.items():
         r["projected_qps"] = m / (r["rank_ms"] * 1e-3)
