@@ -804,16 +804,17 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     const char *np_env = getenv("KNN_NO_PAIR");
     const int can_pair = (c->h16 || c->i8) && 2 * c->lpq * nsplit + 1 <= 64 &&
                          !(np_env && np_env[0] == '1');
-    /* a fused step (the direct exchange's received blocks) starts after the
-     * previous step's merge: that merge publishes the (k+1)-th d^2 of the
-     * blocks folded so far into qthr, so the fused launch -- most of the
-     * rank's work -- filters with it from its first tile instead of
-     * warming every lane list cold (KNN_FUSE_WAIT=0: no wait) */
+    /* a fused step (the direct exchange's received blocks) is never paired:
+     * the previous step's merge runs beside it and publishes the (k+1)-th
+     * d^2 of the blocks folded so far into qthr, which the fused launch's
+     * workgroups re-read as they go (k_dist_topk_i8), so most of the rank's
+     * work filters with the running answer instead of cold lane lists.
+     * KNN_FUSE_WAIT=1: the launch waits for that merge instead. */
     const char *fw_env = getenv("KNN_FUSE_WAIT");
-    const int fuse_wait = xb && c->nstep > 0 && !(fw_env && fw_env[0] == '0');
+    const int fuse_wait = xb && c->nstep > 0 && fw_env && fw_env[0] == '1';
     int pairing = 0;
     if ((set & 1) && c->pend) {
-        pairing = can_pair && nsplit == c->pend_nsplit && !fuse_wait;
+        pairing = can_pair && nsplit == c->pend_nsplit && !xb;
         if (!pairing) RCHK(merge_pending(c));
     }
     {

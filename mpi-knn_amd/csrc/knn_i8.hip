@@ -412,6 +412,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // round; the rounds are dense: a merge runs when some lane's buffer is
     // full, so most lanes insert a real entry every round
     auto merge = [&]() {
+        // the shared bound may have fallen since the workgroup started (the
+        // merge of an earlier ring step publishes the running answer while
+        // a fused launch runs): re-read it, issued here, used after the rounds
+        unsigned long long qb_bits = 0x7ff0000000000000ull;
+        if (W == 8 && qthr != nullptr && h == 0 && myq < nq)   // (the 4-wave kernel has no registers to spare)
+            qb_bits = __hip_atomic_load(qthr + myq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int e = 0; __ballot(e < cnt) != 0ull; e++) {
             int d = I8_INF, id = -1;
             if (e < cnt) {
@@ -422,6 +428,13 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             i8_insert<KL>(L, I, d, id);
         }
         cnt = 0;
+        if constexpr (W == 8) {
+            const double td = __longlong_as_double((long long)qb_bits);
+            int tq = td >= 2147483647.0 ? I8_INF : (int)td;
+            const int tqo = __shfl_xor(tq, 32);
+            tq = tqo < tq ? tqo : tq;
+            thr = tq < thr ? tq : thr;
+        }
         refresh();
     };
 
