@@ -775,11 +775,13 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
             int j = tab.nblk++;
             while (j > 0 && tab.base[j - 1] > xb->base[b]) {
                 tab.ptr[j] = tab.ptr[j - 1];
+                tab.nptr[j] = tab.nptr[j - 1];
                 tab.base[j] = tab.base[j - 1];
                 tab.nc[j] = tab.nc[j - 1];
                 j--;
             }
             tab.ptr[j] = xb->ptr[b];
+            tab.nptr[j] = xb->nptr[b];
             tab.base[j] = xb->base[b];
             tab.nc[j] = xb->nc[b];
         }

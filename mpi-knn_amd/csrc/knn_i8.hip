@@ -166,6 +166,7 @@ __global__ __launch_bounds__(256) void k_shadow8(signed char *__restrict__ dst, 
 // block (wave-uniform LDS reads, made scalar by readfirstlane).
 struct i8_tab_lds {
     unsigned long long ptr[KNN_I8_MAXBLK];
+    unsigned long long nptr[KNN_I8_MAXBLK];
     long long base[KNN_I8_MAXBLK];
     int nc[KNN_I8_MAXBLK];
     int t0[KNN_I8_MAXBLK + 1];
@@ -266,7 +267,6 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     constexpr int NCH = (NKS + 3) / 4;      // chunks a tile
     const int nch = NCH;
     const int *qnorms = (const int *)(qsh + q_rows_pad * (size_t)rs);
-    const size_t cnorm_off = c_rows_pad * (size_t)rs;   // norms behind the rows of every block
 
     // ---- resident query fragments (B), one per K-step --------------------
     // NKS >= nks K-steps (the instantiation's bucket): those past nks get
@@ -316,6 +316,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
 #pragma unroll
         for (int j = 0; j < KNN_I8_MAXBLK; j++) {
             tab->ptr[j] = (unsigned long long)(uintptr_t)cb.ptr[j];
+            tab->nptr[j] = (unsigned long long)(uintptr_t)cb.nptr[j];
             tab->base[j] = cb.base[j];
             tab->nc[j] = cb.nc[j];
         }
@@ -342,6 +343,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     int s_t = t_lo, s_c = 0, s_x = 0;
     int s_b = i8_blk_of(tab, t_lo);
     const signed char *s_ptr = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]);
+    const int *s_nptr = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]);
     int s_t0 = i8_rfl(tab->t0[s_b]), s_t1 = i8_rfl(tab->t0[s_b + 1]);
     auto stage = [&]() {
         const size_t lt = (size_t)(s_t - s_t0);
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         else bglds16x2(i8_rsrc(base), voff[0], voff[1], dst);
         if (s_x < total && s_c == 0) {
             if (lane < 32 / W)
-                bglds16(i8_rsrc((const int *)(s_ptr + cnorm_off) + lt * 128 + (128 / W) * wave_s), 16u * lane,
+                bglds16(i8_rsrc(s_nptr + lt * 128 + (128 / W) * wave_s), 16u * lane,
                         lds0 + NORM0 + (unsigned)(s_t % NST) * 512u + (512u / W) * wave_s);
         }
         s_x++;
@@ -361,6 +363,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 if (++s_t == s_t1) {   // next block of the launch
                     s_b++;
                     s_ptr = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]);
+                    s_nptr = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]);
                     s_t0 = s_t1;
                     s_t1 = i8_rfl(tab->t0[s_b + 1]);
                 }
@@ -666,6 +669,7 @@ extern "C" int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_
     knn_i8_blocks_t cb = *cbp;
     cb.t0[0] = 0;
     for (int b = 0; b < cb.nblk; b++) {
+        if (!cb.nptr[b]) cb.nptr[b] = (const char *)cb.ptr[b] + c_rows_pad * (size_t)rs;
         if (!cb.ptr[b] || cb.nc[b] <= 0 || (size_t)cb.nc[b] > c_rows_pad || cb.base[b] < 0 ||
             (b > 0 && cb.base[b] < cb.base[b - 1] + cb.nc[b - 1]))
             return KNN_ERR_INVALID;
@@ -673,6 +677,7 @@ extern "C" int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_
     }
     for (int b = cb.nblk; b < KNN_I8_MAXBLK; b++) {
         cb.ptr[b] = cb.ptr[cb.nblk - 1];
+        cb.nptr[b] = cb.nptr[cb.nblk - 1];
         cb.base[b] = cb.base[cb.nblk - 1];
         cb.nc[b] = cb.nc[cb.nblk - 1];
         cb.t0[b + 1] = cb.t0[cb.nblk];

@@ -83,10 +83,12 @@ static inline size_t knn_s8_bytes(size_t cap, size_t n)
 /* Corpus blocks of one k_dist_topk_i8 launch (a fused ring step): byte
  * blocks of one capacity, ascending global base (so every lane meets its
  * candidates in increasing row order: the stable tie rule), block b holding
- * global tiles [t0[b], t0[b+1]) of the launch. */
+ * global tiles [t0[b], t0[b+1]) of the launch.  An entry may also be a
+ * whole-tile range of a block: ptr / nptr / base advanced by its first tile. */
 #define KNN_I8_MAXBLK 8
 typedef struct {
-    const void *ptr[KNN_I8_MAXBLK];
+    const void *ptr[KNN_I8_MAXBLK];   /* row 0 of the block (or of a tile range of it) */
+    const void *nptr[KNN_I8_MAXBLK];  /* its norms; NULL: the block's, ptr + cap_pad * row bytes */
     int64_t base[KNN_I8_MAXBLK];
     int nc[KNN_I8_MAXBLK];
     int t0[KNN_I8_MAXBLK + 1];

@@ -26,6 +26,7 @@ static void kb8_go(dim3 grid, const void *qsh, size_t q_rows_pad, int nq, const 
     cb.nblk = 1;
     for (int b = 0; b < KNN_I8_MAXBLK; b++) {
         cb.ptr[b] = csh;
+        cb.nptr[b] = (const char *)csh + c_rows_pad * (size_t)rs;
         cb.nc[b] = nc;
         cb.t0[b + 1] = ntiles;
     }
