@@ -819,6 +819,26 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     }
 }
 
+// One step of a DPP argmin by (d, idx): lanes the row/bank masks leave out,
+// and lanes whose source lies outside their row, see (+inf, INT_MAX)
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ void dpp_argmin_step(double &d, int &i)
+{
+    const int lo = __double2loint(d), hi = __double2hiint(d);
+    const int olo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, BM, false);
+    const int ohi = __builtin_amdgcn_update_dpp(0x7ff00000, hi, CTRL, RM, BM, false);
+    const int oi = __builtin_amdgcn_update_dpp(0x7fffffff, i, CTRL, RM, BM, false);
+    const double od = __hiloint2double(ohi, olo);
+    const bool take = (od < d) || (od == d && oi < i);
+    d = take ? od : d;
+    i = take ? oi : i;
+}
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
 // ---------------------------------------------------------------------------
 // k_merge: one wave per query.  Lane j < lpq*nsplit owns partial list j
 // (lpq lists per query and split: 4 from k_dist_topk, 2 from k_dist_topk_i8),
@@ -888,21 +908,44 @@ __global__ __launch_bounds__(256) void k_merge(
 #pragma unroll
     for (int x = 0; x < NS; x++) { sd[x] = KNN_INF; si[x] = -1; ssrc[x] = 0; spos[x] = 0; }
     for (int r = 0; r <= KP; r++) {
+        // segment argmin of the heads by (d^2, idx): DPP row shifts (the
+        // minimum of each 16-lane row in its lane 15), row broadcasts into
+        // the segment's last lane, read back as scalars -- no LDS permutes
         double wd = hd;
         int wi = hi;
-#pragma unroll
-        for (int off = S / 2; off > 0; off >>= 1) {
-            const double od = __shfl_xor(wd, off);
-            const int oi = __shfl_xor(wi, off);
-            const bool take = (od < wd) || (od == wd && oi < wi);
-            wd = take ? od : wd;
-            wi = take ? oi : wi;
+        dpp_argmin_step<0x111, 0xf, 0xf>(wd, wi);   // row_shr:1
+        dpp_argmin_step<0x112, 0xf, 0xf>(wd, wi);   // row_shr:2
+        dpp_argmin_step<0x114, 0xf, 0xf>(wd, wi);   // row_shr:4
+        dpp_argmin_step<0x118, 0xf, 0xf>(wd, wi);   // row_shr:8
+        dpp_argmin_step<0x142, 0xa, 0xf>(wd, wi);   // row_bcast:15 -> rows 1, 3
+        if constexpr (S == 64) dpp_argmin_step<0x143, 0xc, 0xf>(wd, wi);   // row_bcast:31 -> rows 2, 3
+        {
+            const double d1 = readlane_f64(wd, 63);
+            const int i1 = __builtin_amdgcn_readlane(wi, 63);
+            if constexpr (S == 32) {
+                const double d0 = readlane_f64(wd, 31);
+                const int i0 = __builtin_amdgcn_readlane(wi, 31);
+                wd = seg ? d1 : d0;
+                wi = seg ? i1 : i0;
+            } else {
+                wd = d1;
+                wi = i1;
+            }
         }
         const bool live = wd != KNN_INF;   // this query still has heads
         if (__ballot(live) == 0ull) break;
-        const unsigned long long who = __ballot(live && hd == wd && hi == wi) & segm;
+        const unsigned long long wall = __ballot(live && hd == wd && hi == wi);
+        const unsigned long long who = wall & segm;
         const int wl = who ? __builtin_ctzll(who) : lane;   // wave lane of the winner
-        const int wpos = __shfl(pos, wl);
+        int wpos;
+        if constexpr (S == 32) {
+            const unsigned w0 = (unsigned)wall, w1 = (unsigned)(wall >> 32);
+            const int p0 = __builtin_amdgcn_readlane(pos, w0 ? __builtin_ctz(w0) : 0);
+            const int p1 = __builtin_amdgcn_readlane(pos, w1 ? 32 + __builtin_ctz(w1) : 32);
+            wpos = seg ? p1 : p0;
+        } else {
+            wpos = __builtin_amdgcn_readlane(pos, wall ? __builtin_ctzll(wall) : 0);
+        }
         if (live) {
             if (r < KP) {
                 if (sl == r % S) {
