@@ -848,7 +848,15 @@ __device__ __forceinline__ double readlane_f64(double v, int l)
 // new in this step get their exact reference-order S from the resident
 // block (the only step at which their rows are on this device).
 // ---------------------------------------------------------------------------
-template <typename TE, int KP, int S>
+// PF > 0: each lane's next PF entries are loaded up front, unconditionally
+// (lanes without a list read a +inf list), and shifted as its head is taken;
+// the running state is split over KP / PF lanes (sorted runs of PF), so a
+// lane only goes back to memory after PF wins.  PF = 0: the head is loaded
+// as it is consumed (one memory latency on every one of the KP + 1 rounds).
+__device__ const double k_inf_d[8] = {KNN_INF, KNN_INF, KNN_INF, KNN_INF, KNN_INF, KNN_INF, KNN_INF, KNN_INF};
+__device__ const int k_inf_i[8] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff,
+                                   0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+template <typename TE, int KP, int S, int PF = 0>
 __global__ __launch_bounds__(256) void k_merge(
     const double *__restrict__ part_d, const int *__restrict__ part_i,
     const double *__restrict__ part_T, int nsplit, int lpq, int kl, int nq, int nq_pad, int first_step,
@@ -871,23 +879,49 @@ __global__ __launch_bounds__(256) void k_merge(
     const int mode = knn_mode<TE>(meta, n);
     const int nl = lpq * nsplit;   // partial lists: [split][query][lpq][kl]
 
+    static_assert(PF == 0 || (PF == 8 && KP % PF == 0), "prefetch depth");
+    constexpr int NST = PF > 0 ? KP / PF : 1;   // state lanes
     const double *src_d = nullptr;
     const int *src_i = nullptr;
-    int len = KP;
+    int len = KP, opos0 = 0;   // opos0: the lane's first slot in the old state
     if (qv && sl < nl) {
         const int s = sl / lpq, gg = sl - s * lpq;
         const size_t base = (((size_t)s * nq_pad + q) * lpq + gg) * kl;
         src_d = part_d + base;
         src_i = part_i + base;
         len = kl;
-    } else if (qv && sl == nl && !first_step) {
-        src_d = st_d + (size_t)q * KP;
-        src_i = st_i + (size_t)q * KP;
+    } else if (qv && !first_step && sl >= nl && sl < nl + NST) {
+        opos0 = (sl - nl) * (KP / NST);
+        src_d = st_d + (size_t)q * KP + opos0;
+        src_i = st_i + (size_t)q * KP + opos0;
+        len = KP / NST;
     }
     int pos = 0;
-    double hd = src_d ? src_d[0] : KNN_INF;
-    int hi = src_d ? src_i[0] : 0x7fffffff;
-    if (hd == KNN_INF) hi = 0x7fffffff;
+    constexpr int R = PF > 0 ? PF : 1;
+    double Ld[R];
+    int Li[R];
+    double hd;
+    int hi;
+    if constexpr (PF > 0) {
+        if (!src_d) {
+            src_d = k_inf_d;
+            src_i = k_inf_i;
+            len = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < R; j++) {   // unconditional: one latency for all
+            Ld[j] = src_d[j];
+            Li[j] = src_i[j];
+        }
+#pragma unroll
+        for (int j = 0; j < R; j++) Ld[j] = j < len ? Ld[j] : KNN_INF;
+        hd = Ld[0];
+        hi = hd == KNN_INF ? 0x7fffffff : Li[0];
+    } else {
+        hd = src_d ? src_d[0] : KNN_INF;
+        hi = src_d ? src_i[0] : 0x7fffffff;
+        if (hd == KNN_INF) hi = 0x7fffffff;
+    }
 
     // T: rejection bound of the lane filters (every candidate a lane turned
     // away has d^2 >= T); Td: smallest d^2 dropped by a merge (those rank
@@ -946,6 +980,7 @@ __global__ __launch_bounds__(256) void k_merge(
         } else {
             wpos = __builtin_amdgcn_readlane(pos, wall ? __builtin_ctzll(wall) : 0);
         }
+        if constexpr (PF > 0) wpos += __shfl(opos0, wl);   // state runs: slot in the old state
         if (live) {
             if (r < KP) {
                 if (sl == r % S) {
@@ -954,7 +989,7 @@ __global__ __launch_bounds__(256) void k_merge(
                         if (r / S == x) {
                             sd[x] = wd;
                             si[x] = wi;
-                            ssrc[x] = (wl - seg * S == nl && !first_step) ? 1 : 0;
+                            ssrc[x] = (wl - seg * S >= nl && !first_step) ? 1 : 0;
                             spos[x] = wpos;
                         }
                     }
@@ -964,9 +999,28 @@ __global__ __launch_bounds__(256) void k_merge(
             }
             if (lane == wl) {
                 pos++;
-                hd = (pos < len) ? src_d[pos] : KNN_INF;
-                hi = (pos < len) ? src_i[pos] : 0x7fffffff;
-                if (hd == KNN_INF) hi = 0x7fffffff;
+                if constexpr (PF > 0) {
+#pragma unroll
+                    for (int j = 0; j + 1 < R; j++) {
+                        Ld[j] = Ld[j + 1];
+                        Li[j] = Li[j + 1];
+                    }
+                    Ld[R - 1] = KNN_INF;
+                    if (pos % R == 0 && pos < len) {   // the prefetched run is used up (rare)
+#pragma unroll
+                        for (int j = 0; j < R; j++) {
+                            const int pj = pos + j < len ? pos + j : len - 1;
+                            Ld[j] = pos + j < len ? src_d[pj] : KNN_INF;
+                            Li[j] = src_i[pj];
+                        }
+                    }
+                    hd = Ld[0];
+                    hi = hd == KNN_INF ? 0x7fffffff : Li[0];
+                } else {
+                    hd = (pos < len) ? src_d[pos] : KNN_INF;
+                    hi = (pos < len) ? src_i[pos] : 0x7fffffff;
+                    if (hd == KNN_INF) hi = 0x7fffffff;
+                }
             }
         }
     }
@@ -1708,12 +1762,24 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
     if (lpq < 1 || kl < 1 || lpq * nsplit + 1 > 64 || k <= 0 || k > kp) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
     const size_t qn_off = q_rows_pad * (size_t)np;
-    // two queries a wave when their lists and state fit 32 lanes
-    const int two = lpq * nsplit + 1 <= 32;
+    // prefetched heads (KP = 32: the state as 4 runs of 8) when the lists
+    // and state lanes fit; two queries a wave when they fit 32 lanes
+    const int pf = kp == 32 && kl >= 8 && lpq * nsplit + 4 <= 64 && !getenv("KNN_MERGE_NOPF");
+    const int two = lpq * nsplit + (pf ? 4 : 1) <= 32;
     const dim3 grid((unsigned)((nq + (two ? 7 : 3)) / (two ? 8 : 4)));
     hipStream_t s = (hipStream_t)stream;
 #define CALL(T, KL, KP)                                                                          \
-    if (two)                                                                                     \
+    if (pf && KP == 32 && two)                                                                   \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, 32, 32, 8>), grid, dim3(256), 0, s, part_d,  \
+                           part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
+                           st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
+                           np, meta, k, (unsigned long long *)qthr);                               \
+    else if (pf && KP == 32)                                                                     \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, 32, 64, 8>), grid, dim3(256), 0, s, part_d,  \
+                           part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
+                           st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
+                           np, meta, k, (unsigned long long *)qthr);                               \
+    else if (two)                                                                                \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP, 32>), grid, dim3(256), 0, s, part_d,     \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
                            st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
