@@ -503,6 +503,9 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
     }
     c->lpq = c->i8 ? knn_i8_lpq(c->kp) : 4;
     c->klx = c->i8 ? knn_i8_kl(c->kp) : c->kl;
+    if (c->i8 && c->klx == KNN_I8_KL && getenv("KNN_I8_KL") && atoi(getenv("KNN_I8_KL")) == KNN_I8_KL_S &&
+        4 * KNN_I8_KL_S >= c->k + 1)
+        c->klx = KNN_I8_KL_S;
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
      * element fragments in the kernel instead) */
     c->shadow = c->i8 ? 2 : (c->h16 && !env_on("KNN_NO_SHADOW"));
@@ -643,7 +646,7 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
      * ~1e-3 of the queries uncertified (a lane list held 17 of the k) */
     int s_min = 1;
     if (c->i8) {
-        const int kl = knn_i8_kl(c->kp);
+        const int kl = c->klx;
         s_min = (4 * (c->k + 1) + c->lpq * kl - 1) / (c->lpq * kl);
         if (s_min > smax) s_min = smax;
         if (s_min < 1) s_min = 1;
@@ -876,7 +879,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
             tab.base[0] = (int64_t)c_base;
             tab.nc[0] = (int)nc;
         }
-        RCHK(knn_launch_dist_i8(c->kp, c->k, c->qs8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
+        RCHK(knn_launch_dist_i8(c->kp, c->klx, c->k, c->qs8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
                                 knn_rows_pad(c->block_cap), (int)c->n, nsplit, c->part_d[set],
                                 c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr, ds));
     } else

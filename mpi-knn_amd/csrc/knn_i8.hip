@@ -306,7 +306,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // uj: list slot of the 2-lane bound (low byte) and of the 4-lane bound
     // (W = 8: the query's lanes in both waves; second byte)
     const int ujm = (uj & 255) < KL - 1 ? (uj & 255) : KL - 1;
-    const int uj4 = (uj >> 8) < KL - 1 ? (uj >> 8) : KL - 1;
+    const int uj4 = ((uj >> 8) & 255) < KL - 1 ? ((uj >> 8) & 255) : KL - 1;
     LDS_AS int *xb = (LDS_AS int *)(smem + XB0);
     LDS_AS int *bk = (LDS_AS int *)(smem + BUF0) + wave_s * NB * 64 + lane;   // entry e at bk[64 e]
     LDS_AS int *bi = bk + W * NB * 64;
@@ -402,7 +402,9 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         lmin = lo < lmin ? lo : lmin;
         u = uo > u ? uo : u;
         u4 = u4o > u4 ? u4o : u4;
+        // short lane lists (2 KL < k + 1, uj bit 16): no 2-lane bound
         int nb = lmin < u ? lmin : u;
+        if (uj & (1 << 16)) nb = I8_INF;
         if constexpr (W == 8) {
             if (h == 0) xb[wave_s * 32 + r32] = u4;
             const int pu = xb[(wave_s ^ 4) * 32 + r32];
@@ -655,14 +657,13 @@ static void launch_i8(dim3 grid, hipStream_t s, const void *qsh, size_t q_rows_p
                        nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj);
 }
 
-extern "C" int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_pad, size_t q_base,
+extern "C" int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t q_rows_pad, size_t q_base,
                                   int nq, const knn_i8_blocks_t *cbp, size_t c_rows_pad, int n,
                                   int nsplit, double *part_d, int *part_i, double *part_T,
                                   int nq_pad, double *qthr, void *stream)
 {
     const int rs = (int)knn_s8_rs((size_t)n), nks = rs / 32;
     const int nqb = (nq + 127) / 128;
-    const int kl = knn_i8_kl(kp);
     if (!cbp || cbp->nblk < 1 || cbp->nblk > KNN_I8_MAXBLK) return KNN_ERR_INVALID;
     // the table the kernel walks: block b = tiles [t0[b], t0[b+1]) of its
     // ceil(nc/128) tiles, ascending bases, rows inside the capacity
@@ -687,8 +688,11 @@ extern "C" int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_
     if ((size_t)nqb * 128 > q_rows_pad || nq_pad < nqb * 128) return KNN_ERR_INVALID;
     // lane-list slot of the shared bound: the 2 lanes of a query cover k + 1
     int uj = (k + 1 + 1) / 2 - 1, uj4 = (k + 1 + 3) / 4 - 1;
+    const int no2 = uj > kl - 1;   // 2 lists of kl cannot hold k + 1
     if (uj > kl - 1) uj = kl - 1;
+    if (kl == KNN_I8_KL_S && 4 * kl < k + 1) return KNN_ERR_INVALID;
     uj |= uj4 << 8;
+    if (no2) uj |= 1 << 16;
     const dim3 grid((unsigned)(nqb * nsplit));
     hipStream_t s = (hipStream_t)stream;
 #define I8_ARGS grid, s, qsh, q_rows_pad, q_base, nq, cb, c_rows_pad, rs, nks, ntiles, nsplit, \
@@ -700,15 +704,23 @@ extern "C" int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_
     // tools/probe/kbench8 variants);
     // k <= 128: 4 waves (one a SIMD, 4 m-blocks, 2 lists a query, 512 VGPRs).
     // K-step buckets: the smallest instantiated NKS >= nks
-    if (kl == KNN_I8_KL) {
+    if (kl == KNN_I8_KL_S) {
+        if (nks <= 4) launch_i8<KNN_I8_KL_S, 4, 8, 2, 8, 6>(I8_ARGS);
+        else if (nks <= 8) launch_i8<KNN_I8_KL_S, 8, 8, 2, 8, 6>(I8_ARGS);
+        else if (nks <= 16) launch_i8<KNN_I8_KL_S, 16, 8, 2, 8, 6>(I8_ARGS);
+        else if (nks <= 25) launch_i8<KNN_I8_KL_S, 25, 8, 2, 8, 6>(I8_ARGS);
+        else launch_i8<KNN_I8_KL_S, 28, 8, 2, 8, 6>(I8_ARGS);
+    } else if (kl == KNN_I8_KL) {
         if (nks <= 4) launch_i8<KNN_I8_KL, 4, 8, 2, 8, 6>(I8_ARGS);
         else if (nks <= 8) launch_i8<KNN_I8_KL, 8, 8, 2, 8, 6>(I8_ARGS);
         else if (nks <= 16) launch_i8<KNN_I8_KL, 16, 8, 2, 8, 6>(I8_ARGS);
         else if (nks <= 25) launch_i8<KNN_I8_KL, 25, 8, 2, 8, 6>(I8_ARGS);
         else launch_i8<KNN_I8_KL, 28, 8, 2, 8, 6>(I8_ARGS);
-    } else {
+    } else if (kl == KNN_I8_KL_L) {
         if (nks <= 4) launch_i8<KNN_I8_KL_L, 4, 4, 1, 8, 8>(I8_ARGS);
         else launch_i8<KNN_I8_KL_L, 28, 4, 1, 8, 8>(I8_ARGS);
+    } else {
+        return KNN_ERR_INVALID;
     }
 #undef I8_ARGS
     return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;

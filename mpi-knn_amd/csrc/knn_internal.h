@@ -73,6 +73,7 @@ static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
 #define KNN_I8_MAX_N 896  /* 7 chunks of 128 features: queries stay in VGPRs */
 #define KNN_I8_KL   17    /* per-lane list, k <= 32: 8-wave kernel, 4 lists a query  */
 #define KNN_I8_KL_L 65    /* k <= 128: 4-wave kernel, 2 lists a query (2 KL > k)    */
+#define KNN_I8_KL_S 12    /* k <= 47, KNN_I8_KL=12: short lists (4 KL > k, 4-lane bound only) */
 /* row bytes: whole K-steps of 32 */
 static inline size_t knn_s8_rs(size_t n) { return knn_round_up(n ? n : 1, 32); }
 static inline size_t knn_s8_norm_offset(size_t cap, size_t n) { return knn_rows_pad(cap) * knn_s8_rs(n); }
@@ -122,7 +123,7 @@ int knn_launch_fill_inf(double *p, int count, void *stream);
  * int8 distance + top-k kernel (partial lists [split][query][2][kl]) */
 int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,
                        const double *meta, void *stream);
-int knn_launch_dist_i8(int kp, int k, const void *qsh, size_t q_rows_pad, size_t q_base, int nq,
+int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t q_rows_pad, size_t q_base, int nq,
                        const knn_i8_blocks_t *cb, size_t c_rows_pad, int n, int nsplit,
                        double *part_d, int *part_i, double *part_T, int nq_pad, double *qthr,
                        void *stream);
