@@ -502,10 +502,10 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
         c->h16 = !c->i8 && !no_h16 && knn_h16_exact(h_meta, c->n, c->dtype);
     }
     c->lpq = c->i8 ? knn_i8_lpq(c->kp) : 4;
+    /* int8 lane lists: 12 entries (k <= 32), 17 on request (KNN_I8_KL=17) */
     c->klx = c->i8 ? knn_i8_kl(c->kp) : c->kl;
-    if (c->i8 && c->klx == KNN_I8_KL && getenv("KNN_I8_KL") && atoi(getenv("KNN_I8_KL")) == KNN_I8_KL_S &&
-        4 * KNN_I8_KL_S >= c->k + 1)
-        c->klx = KNN_I8_KL_S;
+    if (c->i8 && c->klx == KNN_I8_KL_S && getenv("KNN_I8_KL") && atoi(getenv("KNN_I8_KL")) == KNN_I8_KL)
+        c->klx = KNN_I8_KL;
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
      * element fragments in the kernel instead) */
     c->shadow = c->i8 ? 2 : (c->h16 && !env_on("KNN_NO_SHADOW"));
@@ -640,14 +640,14 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         smax = KNN_PART_BUDGET / per > 1 ? (int)(KNN_PART_BUDGET / per) : 1;
     const double wgc = c->i8 ? KNN_WG_COST_I8_KSTEPS / (double)(knn_s8_rs(c->n) / 32) : KNN_WG_COST;
     const double mc = c->i8 ? KNN_MERGE_COST_I8 : KNN_MERGE_COST;
-    /* int8 lists: at least s_min splits so that a lane list expects <= KL/4
+    /* int8 lists: at least s_min splits so that a lane list expects <= KL/3
      * of the query's k+1 nearest (lpq lists a split; the block may hold all
      * of them): one split of 17-entry lists over a whole corpus left
      * ~1e-3 of the queries uncertified (a lane list held 17 of the k) */
     int s_min = 1;
     if (c->i8) {
         const int kl = c->klx;
-        s_min = (4 * (c->k + 1) + c->lpq * kl - 1) / (c->lpq * kl);
+        s_min = (3 * (c->k + 1) + c->lpq * kl - 1) / (c->lpq * kl);
         if (s_min > smax) s_min = smax;
         if (s_min < 1) s_min = 1;
     }

@@ -402,9 +402,11 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         lmin = lo < lmin ? lo : lmin;
         u = uo > u ? uo : u;
         u4 = u4o > u4 ? u4o : u4;
-        // short lane lists (2 KL < k + 1, uj bit 16): no 2-lane bound
+        // short lane lists (2 KL < k + 1, uj bit 16): no 2-lane bound.  lmin
+        // stays: thr <= every lane's last entry is what makes the published
+        // T a bound on the candidates a full list drops
         int nb = lmin < u ? lmin : u;
-        if (uj & (1 << 16)) nb = I8_INF;
+        if (uj & (1 << 16)) nb = lmin;
         if constexpr (W == 8) {
             if (h == 0) xb[wave_s * 32 + r32] = u4;
             const int pu = xb[(wave_s ^ 4) * 32 + r32];
@@ -690,7 +692,7 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t
     int uj = (k + 1 + 1) / 2 - 1, uj4 = (k + 1 + 3) / 4 - 1;
     const int no2 = uj > kl - 1;   // 2 lists of kl cannot hold k + 1
     if (uj > kl - 1) uj = kl - 1;
-    if (kl == KNN_I8_KL_S && 4 * kl < k + 1) return KNN_ERR_INVALID;
+    if (4 * kl < k + 1) return KNN_ERR_INVALID;   // the 4-lane bound needs 4 KL >= k + 1
     uj |= uj4 << 8;
     if (no2) uj |= 1 << 16;
     const dim3 grid((unsigned)(nqb * nsplit));

@@ -71,9 +71,10 @@ static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
  * bytes (x - o, o = 128 - meta[MAXNEG]; 0 past n), then one int32 |x - o|^2 per row in
  * the per-tile order of i8_norm_pos, then the block's 8 meta doubles. */
 #define KNN_I8_MAX_N 896  /* 7 chunks of 128 features: queries stay in VGPRs */
-#define KNN_I8_KL   17    /* per-lane list, k <= 32: 8-wave kernel, 4 lists a query  */
+#define KNN_I8_KL_S 12    /* per-lane list, k <= 32: 8-wave kernel, 4 lists a query  */
+                          /* (4 KL >= k + 1: the 4-lane bound; no 2-lane bound)     */
+#define KNN_I8_KL   17    /* the same with 17-entry lists (KNN_I8_KL=17)             */
 #define KNN_I8_KL_L 65    /* k <= 128: 4-wave kernel, 2 lists a query (2 KL > k)    */
-#define KNN_I8_KL_S 12    /* k <= 47, KNN_I8_KL=12: short lists (4 KL > k, 4-lane bound only) */
 /* row bytes: whole K-steps of 32 */
 static inline size_t knn_s8_rs(size_t n) { return knn_round_up(n ? n : 1, 32); }
 static inline size_t knn_s8_norm_offset(size_t cap, size_t n) { return knn_rows_pad(cap) * knn_s8_rs(n); }
@@ -95,7 +96,7 @@ typedef struct {
     int t0[KNN_I8_MAXBLK + 1];
     int nblk;
 } knn_i8_blocks_t;
-static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL : KNN_I8_KL_L; }
+static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL_S : KNN_I8_KL_L; }
 static inline int knn_i8_lpq(int kp) { return kp <= KNN_KP_M ? 4 : 2; }
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
 {

@@ -99,3 +99,24 @@ def test_i8_matches_fp16_path(oracle, monkeypatch):
     b, b16 = run_engine(X, 30, "f64")
     assert (b8, b16) == (8, 16)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("kl", ["12", "17"])
+@pytest.mark.parametrize("case", ["mnist", "digits", "dups", "sift"])
+def test_i8_lane_list_lengths(oracle, monkeypatch, kl, case):
+    """Both lane-list lengths of the k <= 32 kernel (12 by default, 17 with
+    KNN_I8_KL=17): with 12 entries only the 4-lane bound applies (2 x 12 <
+    k + 1) and the published bound must still sit at or below every list's
+    last entry (a full list drops candidates there); heavy ties, mass
+    duplicates and k = 32 over few lanes exercise that."""
+    monkeypatch.setenv("KNN_I8_KL", kl)
+    if case == "mnist":
+        check(oracle, datasets.mnist_like(2500, 784, seed=31)[0], 30)
+    elif case == "digits":
+        check(oracle, datasets.digits()[0], 30)
+    elif case == "dups":
+        rng = np.random.default_rng(8)
+        X = rng.integers(0, 4, (2000, 24)).astype(np.float64)   # massive ties
+        check(oracle, X, 30)
+    else:
+        check(oracle, datasets.sift_like(8000, 128, clusters=16, seed=3), 32, dtype="f32")

@@ -31,7 +31,7 @@ static void kb8_go(dim3 grid, const void *qsh, size_t q_rows_pad, int nq, const 
         cb.t0[b + 1] = ntiles;
     }
     cb.t0[0] = 0;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KNN_I8_KL, NKS, 8, 2, NST, NB>), grid, dim3(512), 0, 0,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KNN_I8_KL_S, NKS, 8, 2, NST, NB>), grid, dim3(512), 0, 0,
                        (const signed char *)qsh, q_rows_pad, (size_t)0, nq, cb, c_rows_pad, rs, nks, ntiles,
                        nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj);
 }
@@ -45,8 +45,10 @@ extern "C" float kbench8(int variant, const void *qsh, size_t q_rows_pad, int nq
     const int rs = (int)knn_s8_rs((size_t)n), nks = rs / 32;
     const int nqb = (nq + 127) / 128, ntiles = (nc + 127) / 128;
     int uj = (k + 2) / 2 - 1, uj4 = (k + 4) / 4 - 1;   // as knn_launch_dist_i8
-    if (uj > KNN_I8_KL - 1) uj = KNN_I8_KL - 1;
+    const int no2 = uj > KNN_I8_KL_S - 1;   // as knn_launch_dist_i8
+    if (uj > KNN_I8_KL_S - 1) uj = KNN_I8_KL_S - 1;
     uj |= uj4 << 8;
+    if (no2) uj |= 1 << 16;
     if (nks > 25) return -1.f;
     const dim3 grid((unsigned)(nqb * nsplit));
     hipEvent_t e0, e1;

@@ -61,7 +61,7 @@ def main():
     nq = a.nq or m
     nq_pad = (nq + 127) // 128 * 128
     rp = (m + 127) // 128 * 128
-    kl = 17   # KNN_I8_KL, 4 lists a query
+    kl = 12   # KNN_I8_KL_S (the product lists), 4 lists a query
     smax = max(int(x) for x in (a.splits or str(splits)).split(","))
     pd = torch.empty(smax * nq_pad * 4 * kl, dtype=torch.float64, device="cuda:0")
     pi = torch.empty(smax * nq_pad * 4 * kl, dtype=torch.int32, device="cuda:0")
