@@ -13,8 +13,8 @@ __global__ void kb8_fill_inf(double *p, int n)
     if (i < n) p[i] = __builtin_inf();
 }
 
-// variant v: (NST, NB) = {0: (7, 8) the product, 1: (8, 6), 2: (8, 4),
-// 3: (7, 6), 4: (7, 4), 5: (8, 5)} at the data's K-step bucket (sift 4,
+// variant v: (NST, NB) = {0: (7, 8), 1: (8, 6), 2: (8, 4),
+// 3: (7, 6), 4: (7, 4), 5: (8, 5) the product} at the data's K-step bucket (sift 4,
 // mnist 25)
 template <int NKS, int NST, int NB>
 static void kb8_go(dim3 grid, const void *qsh, size_t q_rows_pad, int nq, const void *csh, size_t c_rows_pad,

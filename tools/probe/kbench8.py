@@ -3,8 +3,8 @@
   python tools/probe/kbench8.py [--workload mnist|sift] [--iters 5]
          [--variant 0,1] [--splits 4,6] [--m M] [--keep-qthr | --ideal-qthr]
 
-Variant v selects (NST staging stages, NB survivor-buffer entries): 0 (7, 8)
-the product, 1 (8, 6), 2 (8, 4), 3 (7, 6), 4 (7, 4), 5 (8, 5).  Prints one JSON line per (variant,
+Variant v selects (NST staging stages, NB survivor-buffer entries): 0 (7, 8),
+1 (8, 6), 2 (8, 4), 3 (7, 6), 4 (7, 4), 5 (8, 5) the product (12-entry lists).  Prints one JSON line per (variant,
 splits)."""
 import argparse
 import ctypes
