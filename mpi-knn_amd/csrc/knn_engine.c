@@ -653,7 +653,13 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     }
     int best = s_min;
     double best_t = 0.0;
-    for (int s = s_min; s <= smax; s++) {
+    /* short rows (<= 8 K-steps a tile: SIFT's n = 128) with a full grid at
+     * s_min: s_min.  The per-tile epilogue outweighs the contraction there
+     * and every extra split is another set of cold lane lists (emulated
+     * sift P = 8 fused launch: 3 / 4 / 6 / 9 splits 38.2 / 38.9 / 40.2 /
+     * 42.7 ms; the makespan model picked 9) */
+    const int short_rows = c->i8 && knn_s8_rs(c->n) / 32 <= 8 && nqb * s_min >= c->cus;
+    for (int s = s_min; s <= smax && !short_rows; s++) {
         if (s > s_min && ntiles / s < 4) break;
         const double t = launch_makespan(nqb, ntiles, s, c->cus, wgc) + mc * (double)c->nq * s;
         if (s == s_min || t < best_t * (1.0 - 2e-3)) {
