@@ -262,7 +262,8 @@ KNN_API int knn_ctx_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
  * once).  Byte blocks (knn_ctx_shadow == 2) share one distance launch per 8
  * blocks, which counts as ONE step of the lag rule above: none of the
  * blocks may be overwritten before KNN_STEP_LAG further steps (or
- * knn_ctx_end).  fp16 shadow blocks fold one block a step. */
+ * knn_ctx_end).  fp16 shadow blocks fold one block a step (and so do
+ * byte blocks with KNN_NO_FUSE=1). */
 KNN_API int knn_ctx_step_shadow_n(knn_ctx_t *ctx, int nblk, const void *const *d_sblocks,
                                   const size_t *nc, const size_t *c_base, void *stream);
 

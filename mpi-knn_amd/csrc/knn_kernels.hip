@@ -1764,7 +1764,7 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
     const size_t qn_off = q_rows_pad * (size_t)np;
     // prefetched heads (KP = 32: the state as 4 runs of 8) when the lists
     // and state lanes fit; two queries a wave when they fit 32 lanes
-    const int pf = kp == 32 && kl >= 8 && lpq * nsplit + 4 <= 64 && !getenv("KNN_MERGE_NOPF");
+    const int pf = kp == 32 && kl >= 8 && lpq * nsplit + 4 <= 64;
     const int two = lpq * nsplit + (pf ? 4 : 1) <= 32;
     const dim3 grid((unsigned)((nq + (two ? 7 : 3)) / (two ? 8 : 4)));
     hipStream_t s = (hipStream_t)stream;
