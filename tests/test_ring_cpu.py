@@ -1,6 +1,7 @@
 """The per-rank ring driver (mpiknn/ring.py) under gloo on CPU.
 
-world_size 2, 3 and 4 processes run the real ring_search() schedules -- meta
+world_size 2, 3, 4 (and 8 for the direct exchange) processes run the real
+ring_search() schedules -- meta
 all-reduce, then either P-1 isend/irecv hops per pass with the query block
 kept resident ("ring") or one exchange of every block with every rank
 ("direct"), and the rescan pass -- with a CPU stand-in engine whose per-block fold
@@ -93,8 +94,9 @@ def _worker(rank, world, port, force_rescan, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("schedule", ["ring", "direct"])
-@pytest.mark.parametrize("world,force_rescan", [(2, False), (3, True), (4, True)])
+@pytest.mark.parametrize("schedule,world,force_rescan",
+                         [(s, w, f) for s in ("ring", "direct") for w, f in ((2, False), (3, True), (4, True))] +
+                         [("direct", 8, True)])
 def test_ring_schedule_gloo(world, force_rescan, schedule, monkeypatch):
     monkeypatch.setenv("KNN_RING_SCHEDULE", schedule)   # inherited by the spawned ranks
     ctx = mp.get_context("spawn")
