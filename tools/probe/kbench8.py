@@ -93,16 +93,6 @@ def main():
         rec = {"workload": a.workload, "m": m, "nq": nq, "keep_qthr": a.keep_qthr, "ideal": a.ideal_qthr,
                "variant": var, "splits": splits, "ms": ms,
                "tops": flop / (ms * 1e-3) / 1e12 if ms > 0 else None}
-        if os.environ.get("KB8_TIMES"):
-            nwg = ((m + 127) // 128) * splits
-            buf = (ctypes.c_ulonglong * (2 * nwg))()
-            L.kb8_times(buf, nwg)
-            t = np.array(buf[:], dtype=np.int64).reshape(nwg, 2)
-            d = (t[:, 1] - t[:, 0]) / 100.0          # wall_clock64: 100 MHz -> us
-            span = (t[:, 1].max() - t[:, 0].min()) / 100.0
-            rec.update(wg_us_min=float(d.min()), wg_us_avg=float(d.mean()), wg_us_p90=float(np.percentile(d, 90)),
-                       wg_us_max=float(d.max()), span_us=span,
-                       start_spread_us=float((t[:, 0].max() - t[:, 0].min()) / 100.0))
         print(json.dumps(rec), flush=True)
 
 
