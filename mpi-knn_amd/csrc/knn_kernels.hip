@@ -941,7 +941,12 @@ __global__ __launch_bounds__(256) void k_merge(
     int si[NS], ssrc[NS], spos[NS];
 #pragma unroll
     for (int x = 0; x < NS; x++) { sd[x] = KNN_INF; si[x] = -1; ssrc[x] = 0; spos[x] = 0; }
-    for (int r = 0; r <= KP; r++) {
+    // INT mode: the state only needs the k + 1 smallest (exact keys, zeros
+    // never admitted: k_finalize reads the k-th, the publication below the
+    // (k+1)-th, and a later merge's top k + 1 comes from these and its new
+    // lists); Td, the smallest dropped value, is a GEMM-certificate term
+    const int rmax = (mode == KNN_MODE_INT && k + 1 < KP) ? k : KP;
+    for (int r = 0; r <= rmax; r++) {
         // segment argmin of the heads by (d^2, idx): DPP row shifts (the
         // minimum of each 16-lane row in its lane 15), row broadcasts into
         // the segment's last lane, read back as scalars -- no LDS permutes
