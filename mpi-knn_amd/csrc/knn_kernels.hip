@@ -833,6 +833,16 @@ __device__ __forceinline__ void dpp_argmin_step(double &d, int &i)
     d = take ? od : d;
     i = take ? oi : i;
 }
+// the same on packed (d^2 << 32 | idx) keys (INT mode with d^2 < 2^32)
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ void dpp_min_u64_step(unsigned long long &key)
+{
+    const unsigned lo = (unsigned)key, hi = (unsigned)(key >> 32);
+    const unsigned olo = (unsigned)__builtin_amdgcn_update_dpp(-1, (int)lo, CTRL, RM, BM, false);
+    const unsigned ohi = (unsigned)__builtin_amdgcn_update_dpp(-1, (int)hi, CTRL, RM, BM, false);
+    const unsigned long long ok = ((unsigned long long)ohi << 32) | olo;
+    key = ok < key ? ok : key;
+}
 __device__ __forceinline__ double readlane_f64(double v, int l)
 {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
@@ -946,18 +956,35 @@ __global__ __launch_bounds__(256) void k_merge(
     // (k+1)-th, and a later merge's top k + 1 comes from these and its new
     // lists); Td, the smallest dropped value, is a GEMM-certificate term
     const int rmax = (mode == KNN_MODE_INT && k + 1 < KP) ? k : KP;
+    // INT mode with every d^2 below 2^32 ((|q| + |c|)^2 <= 4 max|x|^2 <
+    // 2^32; list keys are exact integers, idx >= 0): argmin on packed keys
+    const bool small_keys = mode == KNN_MODE_INT && 4.0 * meta[KNN_META_MAXNORM] < 4294967295.0;
     for (int r = 0; r <= rmax; r++) {
         // segment argmin of the heads by (d^2, idx): DPP row shifts (the
         // minimum of each 16-lane row in its lane 15), row broadcasts into
         // the segment's last lane, read back as scalars -- no LDS permutes
         double wd = hd;
         int wi = hi;
-        dpp_argmin_step<0x111, 0xf, 0xf>(wd, wi);   // row_shr:1
-        dpp_argmin_step<0x112, 0xf, 0xf>(wd, wi);   // row_shr:2
-        dpp_argmin_step<0x114, 0xf, 0xf>(wd, wi);   // row_shr:4
-        dpp_argmin_step<0x118, 0xf, 0xf>(wd, wi);   // row_shr:8
-        dpp_argmin_step<0x142, 0xa, 0xf>(wd, wi);   // row_bcast:15 -> rows 1, 3
-        if constexpr (S == 64) dpp_argmin_step<0x143, 0xc, 0xf>(wd, wi);   // row_bcast:31 -> rows 2, 3
+        if (small_keys) {
+            // one 64-bit key per head: (d^2, idx) order is u64 order
+            unsigned long long key = hd == KNN_INF ? ~0ull
+                                                   : ((unsigned long long)(unsigned)hd << 32) | (unsigned)hi;
+            dpp_min_u64_step<0x111, 0xf, 0xf>(key);
+            dpp_min_u64_step<0x112, 0xf, 0xf>(key);
+            dpp_min_u64_step<0x114, 0xf, 0xf>(key);
+            dpp_min_u64_step<0x118, 0xf, 0xf>(key);
+            dpp_min_u64_step<0x142, 0xa, 0xf>(key);
+            if constexpr (S == 64) dpp_min_u64_step<0x143, 0xc, 0xf>(key);
+            wd = key == ~0ull ? KNN_INF : (double)(unsigned)(key >> 32);
+            wi = key == ~0ull ? 0x7fffffff : (int)(unsigned)key;
+        } else {
+            dpp_argmin_step<0x111, 0xf, 0xf>(wd, wi);   // row_shr:1
+            dpp_argmin_step<0x112, 0xf, 0xf>(wd, wi);   // row_shr:2
+            dpp_argmin_step<0x114, 0xf, 0xf>(wd, wi);   // row_shr:4
+            dpp_argmin_step<0x118, 0xf, 0xf>(wd, wi);   // row_shr:8
+            dpp_argmin_step<0x142, 0xa, 0xf>(wd, wi);   // row_bcast:15 -> rows 1, 3
+            if constexpr (S == 64) dpp_argmin_step<0x143, 0xc, 0xf>(wd, wi);   // row_bcast:31 -> rows 2, 3
+        }
         {
             const double d1 = readlane_f64(wd, 63);
             const int i1 = __builtin_amdgcn_readlane(wi, 63);
