@@ -19,6 +19,28 @@
  *    (x_qj - x_ij)^2 accumulated in j order in fp64 without FMA; exact
  *    zero distances (the point itself and exact duplicates) excluded; ties
  *    ordered by lower 1-based index; missing slots {INFINITY, 0, 0}.
+ *
+ * Environment switches read by the library (none changes a result; each
+ * selects among exact code paths, for tests and diagnosis):
+ *   KNN_NO_I8=1 / KNN_NO_H16=1 / KNN_NO_SHADOW=1
+ *                         disable the int8 / fp16 contraction / fp16 shadow
+ *                         rows (the next exact contraction in line runs)
+ *   KNN_I8_KL=17          17-entry int8 lane lists instead of 12
+ *   KNN_SPLITS=s          corpus splits per launch instead of the model's
+ *   KNN_NO_FUSE=1         fold received byte blocks one launch each
+ *   KNN_FORCE_RESCAN=1    send every query through the exact rescan pass
+ *   KNN_FORCE_RING=1      knn_search runs the ring driver on one GPU
+ *   KNN_RING_SCHEDULE=ring|direct
+ *                         ring driver schedule: "ring" = the reference's
+ *                         neighbour rotation (blk:187-244), "direct" = every
+ *                         block to every rank at once (default; bit-identical
+ *                         results, tested through the loopback transport and
+ *                         gloo -- no multi-GPU node has run it yet)
+ *   KNN_RING_FUSE=rest|all direct schedule: own block folded beside the
+ *                         exchange (rest) or with the received blocks (all)
+ *   KNN_RING_LOOPBACK=1   P virtual ranks on device 0 (tests)
+ *   KNN_NO_SHADOW_RING=1  ring moves element blocks, not shadow/byte blocks
+ *   KNN_MAT / KNN_MPI_COMPAT  the CLIs: .mat path, bug-compatible mode
  */
 #ifndef KNN_H
 #define KNN_H

@@ -352,15 +352,10 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     c->block_cap = block_cap;
     c->k = k;
     c->kp = knn_kp_for(k, dtype);
-    /* tuning override: an fp32 context may take any variant holding k */
-    if (dtype == KNN_F32 && getenv("KNN_FORCE_KP")) {
-        const int f = atoi(getenv("KNN_FORCE_KP"));
-        if ((f == KNN_KP || f == KNN_KP_M || f == KNN_KP_L) && k <= f) c->kp = f;
-    }
     c->kl = knn_kl_for(c->kp);
     c->lpq = 4;
     c->klx = c->kl;
-    c->xord = getenv("KNN_XCD_ORDER") ? atoi(getenv("KNN_XCD_ORDER")) != 0 : 0;
+    c->xord = 0;   /* split-major (the XCD-grouped order measured no faster) */
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
 
     const size_t np = c->nq_pad;
@@ -811,18 +806,15 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     /* pairing: in exact-integer (fp16) searches two consecutive steps share
      * one k_merge (8*nsplit + 1 <= 64 lists; INT mode never reads the
      * block rows in k_merge) -- half the merges, which at P = 8 cost about
-     * as much as the contraction.  KNN_NO_PAIR=1 disables it. */
-    const char *np_env = getenv("KNN_NO_PAIR");
-    const int can_pair = (c->h16 || c->i8) && 2 * c->lpq * nsplit + 1 <= 64 &&
-                         !(np_env && np_env[0] == '1');
+     * as much as the contraction. */
+    const int can_pair = (c->h16 || c->i8) && 2 * c->lpq * nsplit + 1 <= 64;
     /* a fused step (the direct exchange's received blocks) is never paired:
      * the previous step's merge runs beside it and publishes the (k+1)-th
      * d^2 of the blocks folded so far into qthr, which the fused launch's
      * workgroups re-read as they go (k_dist_topk_i8), so most of the rank's
-     * work filters with the running answer instead of cold lane lists.
-     * KNN_FUSE_WAIT=1: the launch waits for that merge instead. */
-    const char *fw_env = getenv("KNN_FUSE_WAIT");
-    const int fuse_wait = xb && c->nstep > 0 && fw_env && fw_env[0] == '1';
+     * work filters with the running answer instead of cold lane lists
+     * (making the launch wait for that merge measured no faster, DESIGN.md
+     * sec.5). */
     int pairing = 0;
     if ((set & 1) && c->pend) {
         pairing = can_pair && nsplit == c->pend_nsplit && !xb;
@@ -844,10 +836,6 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     HIPCHK(hipEventRecord(c->ev_in, cs));
     HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
     if (c->nstep >= KNN_PSETS) HIPCHK(hipStreamWaitEvent(ds, c->ev_m[set], 0));
-    if (fuse_wait) {
-        if (c->pend) RCHK(merge_pending(c));   /* (pending only at an even set) */
-        HIPCHK(hipStreamWaitEvent(ds, c->ev_m[(c->nstep - 1) % KNN_PSETS], 0));
-    }
     const void *csh = d_sblock, *cn_ptr = NULL;
     if (c->i8) {
         if (!d_sblock && d_cblock == c->qblk && knn_rows_pad(c->block_cap) == c->q_rows_pad) {

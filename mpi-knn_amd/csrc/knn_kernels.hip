@@ -1728,10 +1728,7 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
         // 1; partial lists byte-identical)
         // Every wave stages its own rows (STG 0) for fp64 blocks (mnist 10.0
         // vs 10.1 ms); fp32 (sift) 607 vs 691 ms with waves 0..3 staging.
-        // KNN_STAGE_ALL=0/1 overrides.
-        static const char *sa_env = getenv("KNN_STAGE_ALL");
-        const int stage_all = sa_env ? sa_env[0] == '1' : (int)(sizeof(T) == 8);
-        if (stage_all)
+        if constexpr (sizeof(T) == 8)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 2>), grid, dim3(512), 0, s,
                                (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
                                nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,

@@ -55,8 +55,11 @@ typedef struct {
     size_t rows, base;          /* own block */
     void *qb;                   /* own packed block: the queries, never overwritten */
     void *qs;                   /* own block in the search's shadow form (or NULL) */
-    void **rx;                  /* nrx receive buffers (element-block capacity R):
-                                 * ring NRX, direct P - 1 (rx[j-1] <- block g - j) */
+    void **rx;                  /* nrx receive buffers of rx_bytes each: ring NRX,
+                                 * direct P - 1 (rx[j-1] <- block g - j) */
+    size_t rx_bytes;            /* sized for the form the pass moves (shadow
+                                 * or byte blocks); grown to element blocks
+                                 * only when a rescan needs them */
     void *cur, *nxt;            /* block being folded / being received */
     int hop;                    /* hops made: hop h lands in rx[h % NRX] */
     double *src;                /* raw rows of the own block */
@@ -271,6 +274,27 @@ static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int
     return KNN_OK;
 }
 
+/* Receive buffers of at least `bytes` on device e (all nrx of them).  A
+ * shadow-form pass sizes them for its shadow blocks (a byte block is 1/8 of
+ * an fp64 element block); the rare rescan grows them to element blocks
+ * after the device has drained its streams. */
+static int ensure_rx(ring_dev_t *e, int nrx, size_t bytes)
+{
+    if (e->rx_bytes >= bytes) return KNN_OK;
+    if (hipSetDevice(e->dev) != hipSuccess) return KNN_ERR_HIP;
+    if (e->rx_bytes && (hipStreamSynchronize(e->cs) != hipSuccess || hipStreamSynchronize(e->ms) != hipSuccess))
+        return KNN_ERR_HIP;
+    for (int b = 0; b < nrx; b++) {
+        hipFree(e->rx[b]);
+        e->rx[b] = NULL;
+    }
+    e->rx_bytes = 0;
+    for (int b = 0; b < nrx; b++)
+        if (hipMalloc(&e->rx[b], bytes) != hipSuccess) return KNN_ERR_NOMEM;
+    e->rx_bytes = bytes;
+    return KNN_OK;
+}
+
 /* Largest P' <= P whose ceil(m/P')-row blocks are all non-empty (results do
  * not depend on the block count; the reference CLIs accept any procs). */
 static int ring_blocks_for(size_t m, int P)
@@ -332,8 +356,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             rc = KNN_ERR_HIP;
             break;
         }
-        int rx_ok = (e->rx = (void **)calloc((size_t)nrx, sizeof(void *))) != NULL;
-        for (int b = 0; b < nrx && rx_ok; b++) rx_ok &= hipMalloc(&e->rx[b], bytes) == hipSuccess;
+        const int rx_ok = (e->rx = (void **)calloc((size_t)nrx, sizeof(void *))) != NULL;
         if (!rx_ok || hipMalloc(&e->qb, bytes) != hipSuccess ||
             hipMalloc((void **)&e->src, e->rows * n * sizeof(double)) != hipSuccess ||
             hipMalloc((void **)&e->meta, KNN_META_DOUBLES * sizeof(double)) != hipSuccess ||
@@ -362,7 +385,6 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         hipSetDevice(e->dev);
         e->cur = e->qb;
         e->hop = 0;
-        e->nxt = e->rx[0];
         rc = knn_block_pack_dt(e->qb, dtype, R, e->rows, n, e->src, KNN_F64,
                                layout == KNN_COLMAJOR ? e->rows : n, layout, e->cs);
         if (!rc && hipMemcpyAsync(e->meta, (char *)e->qb + knn_block_meta_offset_dt(R, n, dtype),
@@ -414,6 +436,8 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             if (!rc) rc = knn_ctx_shadow_pack(d[g].ctx, d[g].qs, d[g].qb, R, d[g].cs);
             d[g].cur = d[g].qs;
         }
+        if (!rc) rc = ensure_rx(&d[g], nrx, form ? knn_ctx_shadow_bytes(d[g].ctx, R) : bytes);
+        d[g].nxt = d[g].rx[0];
         if (!rc && hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
     }
     if (!rc && direct)
@@ -435,6 +459,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             hipSetDevice(d[g].dev);
             if (hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
         }
+        for (int g = 0; g < P && !rc; g++) rc = ensure_rx(&d[g], nrx, bytes);
         if (!rc && direct) {
             /* element blocks: exchanged again after a shadow-form pass (the
              * receive buffers held shadow blocks), else still resident */

@@ -74,6 +74,12 @@ class GpuEngine:
         """src: this rank's rows on the device, (rows, n) float64 or float32
         (any strides matching the layout: col-major -> src.t() contiguous)."""
         rows = src.shape[0]
+        if rows == 0:
+            # a rank past the last row (m < P * ceil(m/P) - R): no queries,
+            # an empty block; meta 0 is neutral for the MAX all-reduce
+            self.qb.zero_()
+            self.meta.zero_()
+            return
         if layout_col:
             assert src.stride(0) == 1
             ld = src.stride(1)
@@ -216,7 +222,9 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
                 reqs = dist.batch_isend_irecv(ops)
             b = (rank - off - s) % P
             base, rows = blocks[b]
-            if use_shadow:
+            if rows == 0:
+                pass   # an empty block (partition: m < P * R) is not folded
+            elif use_shadow:
                 engine.step_shadow(state["cur"], rows, base)
             else:
                 engine.step(state["cur"], rows, base, rescan)
@@ -266,8 +274,8 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
         fuse = os.environ.get("KNN_RING_FUSE", "rest")
         fuse_all = (use_shadow and fuse == "all" and P > 1 and resident is None and
                     engine.ctx.shadow() == 2)
-        if fuse_all:
-            pass
+        if fuse_all or rows == 0:
+            pass   # (an empty own block is not folded)
         elif use_shadow:
             engine.step_shadow(own, rows, base)
         else:
@@ -283,13 +291,17 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
         else:
             fold = land
         bs = [blocks[b] for b in peers]
+        # empty blocks (m < P * R leaves the last ranks without rows) are
+        # exchanged like the others but never folded
+        nz = [(buf, b, r) for buf, (b, r) in zip(fold, bs) if r > 0]
         if fuse_all:
-            engine.step_shadow_n([own] + list(fold), [rows] + [r for _, r in bs],
-                                 [base] + [b for b, _ in bs])
-        elif use_shadow and len(fold) > 0:
-            engine.step_shadow_n(fold, [r for _, r in bs], [b for b, _ in bs])
+            if rows > 0:
+                nz = [(own, base, rows)] + nz
+            engine.step_shadow_n([x for x, _, _ in nz], [r for _, _, r in nz], [b for _, b, _ in nz])
+        elif use_shadow and len(nz) > 0:
+            engine.step_shadow_n([x for x, _, _ in nz], [r for _, _, r in nz], [b for _, b, _ in nz])
         else:
-            for buf, (b, r) in zip(fold, bs):
+            for buf, b, r in nz:
                 engine.step(buf, r, b, rescan)
         return None if use_shadow else fold
 

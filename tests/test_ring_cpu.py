@@ -36,7 +36,7 @@ class CpuEngine:
         self.qb.zero_()
         self.qb[:rows, : self.n] = src
         self.qb[0, self.n] = rows
-        self.meta[0] = float(src.abs().max())
+        self.meta[0] = float(src.abs().max()) if rows else 0.0
 
     def begin(self, q_base, h_meta=None):
         self.q_base = q_base
@@ -65,7 +65,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, force_rescan, q):
+def _worker(rank, world, port, force_rescan, q, m_rows=None):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.join(here, "..", "oracle"), os.path.join(here, "..", "mpi-knn_amd")):
@@ -78,6 +78,8 @@ def _worker(rank, world, port, force_rescan, q):
         import oracle
         from mpiknn.ring import partition, ring_search
         X, _ = datasets.digits_real()
+        if m_rows:
+            X = np.ascontiguousarray(X[:m_rows])
         m, n = X.shape
         R, blocks = partition(m, world)
         base, rows = blocks[rank]
@@ -86,8 +88,9 @@ def _worker(rank, world, port, force_rescan, q):
         ring_search(dist, torch, eng, rank, world, m, base)
         full = oracle.knn(X, 30, rows=(base, rows))
         ok = np.array_equal(eng.lists[["distance", "idx"]], full[["distance", "idx"]])
-        every = sorted(eng.visits[False]) == sorted(b for b, _ in blocks)
-        every_rescan = (not force_rescan) or sorted(eng.visits[True]) == sorted(b for b, _ in blocks)
+        nonempty = sorted(b for b, r in blocks if r > 0)
+        every = sorted(eng.visits[False]) == nonempty
+        every_rescan = (not force_rescan) or sorted(eng.visits[True]) == nonempty
         meta_ok = float(eng.meta[0]) == float(np.abs(X).max())
         q.put((rank, ok, every, every_rescan, meta_ok))
     finally:
@@ -121,3 +124,24 @@ def test_partition_covers_all_rows():
         R, blocks = partition(m, P)
         assert sum(r for _, r in blocks) == m
         assert all(b == i * R for i, (b, _) in enumerate(blocks))
+
+
+@pytest.mark.parametrize("schedule", ["ring", "direct"])
+def test_ring_empty_last_block_gloo(schedule, monkeypatch):
+    """m = 9 rows over P = 4 ranks: R = 3, so rank 3 owns no rows and its
+    block is empty.  It still joins every exchange; nobody folds it."""
+    monkeypatch.setenv("KNN_RING_SCHEDULE", schedule)
+    from mpiknn.ring import partition
+    assert partition(9, 4)[1][3] == (9, 0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 4
+    procs = [ctx.Process(target=_worker, args=(r, world, port, True, q, 9)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, every, every_rescan, meta_ok in sorted(res):
+        assert ok and every and every_rescan and meta_ok, rank

@@ -41,7 +41,7 @@ run_step() {
   trace)
     (cd /tmp && export TMPDIR=/tmp && cd "$ROOT" &&
      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/trace_$a" -o run -- \
-       python3 bench.py --workload "$a" --no-cpu-baseline --check 0 --steps 5 --warmup 2 \
+       python3 bench.py --workload "$a" --no-cpu-baseline --secondary-steps 0 --check 0 --steps 5 --warmup 2 \
        > "gpurun_out/trace_$a.log" 2>&1) || fail "$spec" $? ;;
   pmc)
     local rep=${b:-3} i g
@@ -51,10 +51,26 @@ run_step() {
         tag=$(echo "$g" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
         (cd /tmp && export TMPDIR=/tmp && cd "$ROOT" &&
          timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/pmc_$a/${tag}_$i" -o run \
-           --pmc $g -- python3 bench.py --workload "$a" --no-cpu-baseline --check 0 --steps 1 --warmup 0 \
+           --pmc $g -- python3 bench.py --workload "$a" --no-cpu-baseline --secondary-steps 0 --check 0 --steps 1 --warmup 0 \
            > "gpurun_out/pmc_$a/${tag}_$i.log" 2>&1) || fail "$spec:$tag:$i" $?
       done
     done ;;
+  pmcx)
+    # one SQ counter group per run (slots: 8 SQ, 2 GRBM): instruction mix,
+    # cycle buckets or LDS; one bench step, the distance kernel's dispatch
+    local cs
+    case $b in
+    inst) cs="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_INSTS_SMEM GRBM_GUI_ACTIVE" ;;
+    cyc) cs="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE" ;;
+    lds) cs="SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_BUSY_CYCLES SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE" ;;
+    *) echo "unknown pmcx group $b"; exit 2 ;;
+    esac
+    mkdir -p "gpurun_out/pmcx_$a"
+    (cd /tmp && export TMPDIR=/tmp && cd "$ROOT" &&
+     timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/pmcx_$a/$b" -o run \
+       --pmc $cs -- python3 bench.py --workload "$a" --no-cpu-baseline --secondary-steps 0 --check 0 --steps 1 --warmup 0 \
+       > "gpurun_out/pmcx_$a/$b.log" 2>&1) || fail "$spec" $?
+    python3 tools/pmc_breakdown.py "gpurun_out/pmcx_$a/$b" ;;
   emu)
     local es fz sw
     es=$(echo "$spec" | cut -s -d: -f4)
