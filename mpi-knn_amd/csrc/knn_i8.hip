@@ -34,6 +34,68 @@ __device__ __forceinline__ int i8_norm_pos(int r)
     return (r & ~127) + (((b * 2 + h) * 4 + j) * 4 + i);
 }
 
+// The norm word of row r is not |x'|^2 itself but the epilogue's addend
+//     K(r) = 31 - slot(r) - 32 |x'|^2,
+// slot(r) = 16 (b & 1) + 4 j + i: the row's position among the 32
+// accumulator registers of a pair of m-blocks (the lane's candidates in one
+// epilogue group), increasing with the row.  With A = q'.c' from the MFMA,
+//     v = 64 A + K = 32 (|q'|^2 - d^2) + (31 - slot)
+// orders the lane's candidates by (d^2, row) in ONE signed integer: the
+// lane's largest v is its nearest candidate, lowest row first on ties
+// (SURVEY F1), and d^2 = |q'|^2 - (v >> 5), slot = 31 - (v & 31) come back
+// out of it.  |x'|^2 = -(K >> 5).  Ranges (n <= 896 bytes, |x'| <= 128, d^2
+// <= n 255^2): |v| < 2^31, and inside one lane (one query) the values span
+// less than 32 (n 255^2 + 1) < 2^31 (i8_next).
+__device__ __forceinline__ int i8_norm_word(int r, int nrm)
+{
+    const int rr = r & 127, b = rr >> 5, w = rr & 31;
+    const int slot = 16 * (b & 1) + 4 * (w >> 3) + (w & 3);
+    return 31 - slot - 32 * nrm;
+}
+__device__ __forceinline__ int i8_max3(int a, int b, int c)
+{
+    int r;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ unsigned i8_min3u(unsigned a, unsigned b, unsigned c)
+{
+    unsigned r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// max of 32 values (a pair of m-blocks' accumulators): 16 v_max3
+__device__ __forceinline__ int i8_max32(const int *v)
+{
+    int m[11];
+#pragma unroll
+    for (int y = 0; y < 10; y++) m[y] = i8_max3(v[3 * y], v[3 * y + 1], v[3 * y + 2]);
+    m[10] = v[30] > v[31] ? v[30] : v[31];
+    const int a = i8_max3(m[0], m[1], m[2]), b = i8_max3(m[3], m[4], m[5]);
+    const int c = i8_max3(m[6], m[7], m[8]), d = i8_max3(m[9], m[10], a);
+    return i8_max3(b, c, d);
+}
+// the largest of the 32 values below vm, or `none` if there is none: the
+// unsigned minimum of vm - 1 - v.  Values below vm map to [0, span) and the
+// rest to [2^32 - span, 2^32) with span < 2^31 (the lane's values span less
+// than 2^31, above), so the two never mix
+__device__ __forceinline__ int i8_next(const int *v, int vm, int none)
+{
+    const unsigned c = (unsigned)vm - 1u;
+    unsigned m[11];
+#pragma unroll
+    for (int y = 0; y < 10; y++) m[y] = i8_min3u(c - (unsigned)v[3 * y], c - (unsigned)v[3 * y + 1],
+                                                 c - (unsigned)v[3 * y + 2]);
+    {
+        const unsigned a = c - (unsigned)v[30], b = c - (unsigned)v[31];
+        m[10] = a < b ? a : b;
+    }
+    const unsigned a = i8_min3u(m[0], m[1], m[2]), b = i8_min3u(m[3], m[4], m[5]);
+    const unsigned cc = i8_min3u(m[6], m[7], m[8]), d = i8_min3u(m[9], m[10], a);
+    const unsigned u = i8_min3u(b, cc, d);
+    return (int)u < 0 ? none : (int)(c - u);
+}
+
 // Insert (d, id) into the ascending register list L (after equal keys: the
 // lane's candidates arrive in row order, so ties keep the lower index,
 // SURVEY F1); d >= L[KL-1] is a no-op.  Keys: L'[e] = med3(L[e-1], L[e], d)
@@ -103,16 +165,8 @@ __device__ __forceinline__ knn_v4i i8_rsrc(const void *base)
     return (knn_v4i){__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y), r.z, r.w};
 }
 
-// a where the lane's bit of m is clear, b where it is set
-__device__ __forceinline__ int i8_sel(unsigned long long m, int a, int b)
-{
-    int r;
-    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
-    return r;
-}
-
 // One wave per row: x' = x - o (0 past n), |x'|^2 reduced in int32 (exact:
-// n 128^2 < 2^31).  Lane l converts the 8-element groups l, l + 64, ... of
+// n 128^2 < 2^31) and stored as the epilogue's norm word (i8_norm_word).  Lane l converts the 8-element groups l, l + 64, ... of
 // the row: 16-byte vector loads (a wave reads 64 contiguous groups), one
 // 8-byte store.  o from the REDUCED meta, so every block of one search
 // shifts alike.
@@ -156,7 +210,7 @@ __global__ __launch_bounds__(256) void k_shadow8(signed char *__restrict__ dst, 
             *(u2 *)(dst + r * (size_t)rs + j0) = (u2){lo, hi};
         }
         for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-        if (lane == 0) norms[i8_norm_pos((int)r)] = s;
+        if (lane == 0) norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, s);
     }
 }
 
@@ -281,7 +335,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             qf[s] = s < nks ? v : (knn_v4i){0, 0, 0, 0};
         }
     }
-    const int qn = qnorms[i8_norm_pos(myq)];
+    const int qn = -(qnorms[i8_norm_pos(myq)] >> 5);   // |q'|^2 (i8_norm_word)
     // shared per-query bound across splits and ring steps (qthr: bits of a
     // non-negative double, atomicMin).  INT-mode bounds are integers, or the
     // next double above one (strict publication), so floor() is the int bound.
@@ -338,34 +392,39 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         voff[p] = (unsigned)(rr * rs + 16 * ((lane & 7) ^ ((rr >> 1) & 7)));
     }
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
-    // staging position: global tile s_t (block s_b, tile s_t - t0[s_b] of it),
-    // chunk s_c; wave-uniform, so the block lookups are scalar selects
-    int s_t = t_lo, s_c = 0, s_x = 0;
+    // staging position: global tile s_t of block s_b, chunk byte offset
+    // s_coff; s_row / s_nrow point at the tile's row 0 / first norm word and
+    // advance by a tile at a time (wave-uniform: scalar registers)
+    int s_t = t_lo, s_x = 0;
+    unsigned s_coff = 0;
     int s_b = i8_blk_of(tab, t_lo);
-    const signed char *s_ptr = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]);
-    const int *s_nptr = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]);
-    int s_t0 = i8_rfl(tab->t0[s_b]), s_t1 = i8_rfl(tab->t0[s_b + 1]);
+    const int s_t0 = i8_rfl(tab->t0[s_b]);
+    int s_t1 = i8_rfl(tab->t0[s_b + 1]);
+    const signed char *s_row = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]) +
+                               (size_t)(t_lo - s_t0) * 128 * rs;
+    const int *s_nrow = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]) + (size_t)(t_lo - s_t0) * 128;
     auto stage = [&]() {
-        const size_t lt = (size_t)(s_t - s_t0);
-        const signed char *base = s_ptr + lt * 128 * rs + 128 * s_c;
-        const unsigned dst = lds0 + (unsigned)(s_x % NST) * 16384u + (unsigned)wave_s * (16384u / W);
-        if constexpr (PW == 4) bglds16x4(i8_rsrc(base), voff[0], voff[1], voff[2], voff[3], dst);
-        else bglds16x2(i8_rsrc(base), voff[0], voff[1], dst);
-        if (s_x < total && s_c == 0) {
+        const unsigned dst = lds0 + ((unsigned)s_x % NST) * 16384u + (unsigned)wave_s * (16384u / W);
+        if constexpr (PW == 4) bglds16x4(i8_rsrc(s_row + s_coff), voff[0], voff[1], voff[2], voff[3], dst);
+        else bglds16x2(i8_rsrc(s_row + s_coff), voff[0], voff[1], dst);
+        if (s_x < total && s_coff == 0) {
             if (lane < 32 / W)
-                bglds16(i8_rsrc(s_nptr + lt * 128 + (128 / W) * wave_s), 16u * lane,
-                        lds0 + NORM0 + (unsigned)(s_t % NST) * 512u + (512u / W) * wave_s);
+                bglds16(i8_rsrc(s_nrow + (128 / W) * wave_s), 16u * lane,
+                        lds0 + NORM0 + ((unsigned)s_t % NST) * 512u + (512u / W) * wave_s);
         }
         s_x++;
         if (s_x < total) {
-            if (++s_c == nch) {
-                s_c = 0;
+            s_coff += 128;
+            if (s_coff == 128u * nch) {
+                s_coff = 0;
                 if (++s_t == s_t1) {   // next block of the launch
                     s_b++;
-                    s_ptr = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]);
-                    s_nptr = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]);
-                    s_t0 = s_t1;
+                    s_row = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]);
+                    s_nrow = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]);
                     s_t1 = i8_rfl(tab->t0[s_b + 1]);
+                } else {
+                    s_row += (size_t)128 * rs;
+                    s_nrow += 128;
                 }
             }
         }
@@ -377,7 +436,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     };
     // A fragments (MB m-blocks) of K-step ks of staged chunk xx
     auto rdA = [&](int xx, int ks, knn_v4i (&a)[MB]) {
-        const LDS_AS char *p = (const LDS_AS char *)smem + (xx % NST) * 16384 + (MB * rh * 32 + r32) * 128 +
+        const LDS_AS char *p = (const LDS_AS char *)smem + ((unsigned)xx % NST) * 16384 + (MB * rh * 32 + r32) * 128 +
                                16 * ((2 * ks + h) ^ ((r32 >> 1) & 7));
 #pragma unroll
         for (int bb = 0; bb < MB; bb++) a[bb] = *(const LDS_AS knn_v4i *)(p + bb * 4096);
@@ -419,12 +478,6 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // round; the rounds are dense: a merge runs when some lane's buffer is
     // full, so most lanes insert a real entry every round
     auto merge = [&]() {
-        // the shared bound may have fallen since the workgroup started (the
-        // merge of an earlier ring step publishes the running answer while
-        // a fused launch runs): re-read it, issued here, used after the rounds
-        unsigned long long qb_bits = 0x7ff0000000000000ull;
-        if (W == 8 && qthr != nullptr && h == 0 && myq < nq)   // (the 4-wave kernel has no registers to spare)
-            qb_bits = __hip_atomic_load(qthr + myq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int e = 0; __ballot(e < cnt) != 0ull; e++) {
             int d = I8_INF, id = -1;
             if (e < cnt) {
@@ -435,14 +488,33 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             i8_insert<KL>(L, I, d, id);
         }
         cnt = 0;
-        if constexpr (W == 8) {
-            const double td = __longlong_as_double((long long)qb_bits);
-            int tq = td >= 2147483647.0 ? I8_INF : (int)td;
-            const int tqo = __shfl_xor(tq, 32);
-            tq = tqo < tq ? tqo : tq;
-            thr = tq < thr ? tq : thr;
-        }
         refresh();
+    };
+    // The shared bound may fall while the workgroup runs (other splits end,
+    // and the merge of an earlier ring step publishes the running answer
+    // while a fused launch runs), so W = 8 workgroups re-read it about once
+    // a tile.  The load is issued from asm, invisible to the compiler's wait
+    // pass: a plain load made it drain every LDS-DMA piece in flight
+    // (vmcnt(0)) before the value's first use.  It is complete once the ring
+    // has waited past the pieces staged after it (wait_next: all but the
+    // NST - 3 youngest chunks), i.e. after chunk q_ready; only then is the
+    // value laundered (asm "+v", ordered after those waits) and used.  A
+    // load issued with s_x = X0 stages out is older than stage X0's pieces;
+    // at an epilogue with xdone > X0 the wait before barrier B(xdone) (or,
+    // on the last tile, B(total - 1) >= X0) has seen stage X0 land.
+    unsigned long long q_bits = 0x7ff0000000000000ull;
+    int q_ready = -1;   // -1: no load pending
+    auto qthr_issue = [&](int xnow) {
+        const unsigned long long *pq = qthr + myq;
+        asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(q_bits) : "v"(pq) : "memory");
+        q_ready = xnow;
+    };
+    auto qthr_apply = [&]() {
+        asm volatile("" : "+v"(q_bits));
+        const double td = __longlong_as_double((long long)q_bits);
+        const int tq = td >= 2147483647.0 ? I8_INF : (int)td;
+        thr = tq < thr ? tq : thr;
+        q_ready = -1;
     };
 
     // ---- epilogue of tile t --------------------------------------------------
@@ -450,89 +522,71 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // first global id and rows (kept by the main loop)
     long c_base = 0;
     int nc = 0, e_t0 = 0, e_t1 = 0, e_b = 0;
-    auto epilogue = [&](int t, knn_v16i (&A)[MB]) {
+    // Survivors are the candidates with d^2 <= lim = min(own KL-th, shared
+    // bound), i.e. v >= T = 32 (|q'|^2 - lim) (i8_norm_word).  An empty
+    // list (lim = INF) admits every real candidate: T = 32 (|q'|^2 - DMAX)
+    // with DMAX above every d^2 (n 255^2 < DMAX); masked slots take
+    // vnone = T_open - 1, below every threshold.
+    const int dmax = rs * 65025 + 1;
+    const int t_open = 32 * (qn - dmax), vnone = t_open - 1;
+    auto thr_v = [&]() -> int {
+        const int lim = L[KL - 1] < thr ? L[KL - 1] : thr;
+        return lim >= dmax ? t_open : 32 * (qn - lim);
+    };
+    auto epilogue = [&](int t, knn_v16i (&A)[MB], int xdone) {
         const int lt = t - e_t0;
         const LDS_AS knn_v4i *cn =
-            (const LDS_AS knn_v4i *)((LDS_AS char *)smem + NORM0 + (t % NST) * 512) + 4 * h + 8 * MB * rh;
-        const int lim = L[KL - 1] < thr ? L[KL - 1] : thr;
-        const int limq = lim == I8_INF ? I8_INF : lim - qn;
-        int lmn = I8_INF;
-#pragma unroll
-        for (int b = 0; b < MB; b++) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const knn_v4i c4 = cn[8 * b + j];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int v = c4[i] - 2 * A[b][4 * j + i];
-                    A[b][4 * j + i] = v;
-                    lmn = v < lmn ? v : lmn;
-                }
-            }
-        }
+            (const LDS_AS knn_v4i *)((LDS_AS char *)smem + NORM0 + ((unsigned)t % NST) * 512) + 4 * h + 8 * MB * rh;
         const int row0 = lt * 128 + 32 * MB * rh;
         const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 32 * qg;
         const bool masked = (row0 + 32 * MB > nc) || (gw0 < gt0 + 32 * MB && gt0 < gw0 + 32);
-        if (!masked && __ballot(lmn <= limq) == 0ull) return;   // common late in the scan
         const int idb = (int)(c_base + row0) + 4 * h;
-        // survivors of G m-blocks at a time (W = 8: both, one 32-bit mask):
-        // one wave round per survivor of the busiest lane; each lane takes its
-        // lowest pending candidate (lowest row: the stable tie order) through
-        // a select tree -- v_cndmask on ballot masks (as plain selects LLVM
-        // folds the tree into a dynamic index: a scratch round trip) -- into
-        // the KL-entry insertion network
-        constexpr int G = W == 8 ? 2 : 1;
+        if constexpr (W == 8) {
+            if (qthr != nullptr) {
+                if (q_ready >= 0 && xdone > q_ready) qthr_apply();
+                if (q_ready < 0) qthr_issue(s_x);
+            }
+        }
+        int T = thr_v();
+        // groups of 2 m-blocks = 32 candidates a lane, lower rows first (the
+        // stable tie order across groups; inside one, v orders by row)
 #pragma unroll
-        for (int g0 = 0; g0 < MB; g0 += G) {
-            unsigned pend = 0;
+        for (int g = 0; g < MB / 2; g++) {
+            int v[32];
 #pragma unroll
-            for (int x = 0; x < 16 * G; x++) pend |= (A[g0 + (x >> 4)][x & 15] <= limq) ? (1u << x) : 0u;
-            if (masked) {
+            for (int bb = 0; bb < 2; bb++)
 #pragma unroll
-                for (int x = 0; x < 16 * G; x++) {
-                    const int r = x & 15, rloc = 32 * (g0 + (x >> 4)) + 8 * (r >> 2) + (r & 3);
-                    if (!(row0 + rloc + 4 * h < nc && idb + rloc != gq)) pend &= ~(1u << x);
+                for (int j = 0; j < 4; j++) {
+                    const knn_v4i c4 = cn[8 * (2 * g + bb) + j];
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        v[16 * bb + 4 * j + i] = (int)((unsigned)A[2 * g + bb][4 * j + i] * 64u + (unsigned)c4[i]);
+                }
+            if (masked) {   // rows past the block, and the query itself
+#pragma unroll
+                for (int x = 0; x < 32; x++) {
+                    const int rloc = 32 * (2 * g + (x >> 4)) + 8 * ((x >> 2) & 3) + (x & 3);
+                    if (!(row0 + rloc + 4 * h < nc && idb + rloc != gq)) v[x] = vnone;
                 }
             }
-            // one survivor at most in every lane (the common case once the
-            // bounds are tight) and no buffer filling up: the survivor is the
-            // lane minimum, so no select tree and no merge (a second merge
-            // site costs ~34 VGPRs)
-            const bool one = G == MB && !masked &&
-                             __ballot(__popc(pend) > 1 || (pend != 0 && cnt == NB - 1)) == 0ull;
-            if (one) {
-                if (pend) {
-                    const int x = __builtin_ctz(pend), r = x & 15;
-                    bk[64 * cnt] = lmn + qn;
-                    bi[64 * cnt] = idb + 32 * (x >> 4) + 8 * (r >> 2) + (r & 3);
+            int vm = i8_max32(v);
+            if (__ballot(vm >= T) == 0ull) continue;   // common late in the scan
+            // survivors in (d^2, row) order, one a round per lane: into the
+            // lane's LDS buffer (NB entries); a full buffer anywhere merges
+            // the wave's buffers into the lists (dense insertion rounds)
+            do {
+                if (vm >= T) {
+                    const int slot = 31 - (vm & 31);
+                    bk[64 * cnt] = qn - (vm >> 5);   // d^2 (0 = a duplicate: dropped at the merge)
+                    bi[64 * cnt] = idb + 32 * (2 * g + (slot >> 4)) + 8 * ((slot >> 2) & 3) + (slot & 3);
                     cnt++;
                 }
-                pend = 0;
-            }
-            while (__ballot(pend != 0) != 0ull) {
-                const int x = pend ? __builtin_ctz(pend) : 0;
-                int v[8 * G];
-                {
-                    const unsigned long long m0 = __ballot(x & 1);
-#pragma unroll
-                    for (int y = 0; y < 8 * G; y++)
-                        v[y] = i8_sel(m0, A[g0 + (y >> 3)][(2 * y) & 15], A[g0 + (y >> 3)][(2 * y + 1) & 15]);
+                if (__ballot(cnt == NB) != 0ull) {
+                    merge();
+                    T = thr_v();
                 }
-#pragma unroll
-                for (int lv = 1, wdt = 8 * G; wdt > 1; lv++, wdt >>= 1) {
-                    const unsigned long long ml = __ballot((x >> lv) & 1);
-#pragma unroll
-                    for (int y = 0; y < wdt / 2; y++) v[y] = i8_sel(ml, v[2 * y], v[2 * y + 1]);
-                }
-                if (pend) {
-                    const int r = x & 15;
-                    bk[64 * cnt] = v[0] + qn;
-                    bi[64 * cnt] = idb + 32 * (g0 + (x >> 4)) + 8 * (r >> 2) + (r & 3);
-                    cnt++;
-                }
-                pend &= pend - 1;
-                if (__ballot(cnt == NB) != 0ull) merge();
-            }
+                vm = i8_next(v, vm, vnone);
+            } while (__ballot(vm >= T) != 0ull);
         }
     };
 
@@ -572,6 +626,11 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                     if (ks < kt) {
                         if (ks + 1 < kt) {
                             rdA(x, ks + 1, anxt);
+                            // keep the reads ahead of this K-step's MFMAs:
+                            // left alone, the scheduler sinks them behind the
+                            // MFMAs into the same registers, and each MFMA
+                            // pair then waited out a ds_read's latency
+                            __builtin_amdgcn_sched_barrier(0);
                         } else if (x + 1 < total) {
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x + 1)
@@ -588,9 +647,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 }
                 x++;
             }
-            epilogue(t, acc);
+            epilogue(t, acc, x);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA left in flight
+        if constexpr (W == 8) {
+            if (q_ready >= 0) qthr_apply();
+        }
     }
     merge();
 
