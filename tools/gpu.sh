@@ -13,6 +13,7 @@
 #                         work; FUSE none|rest|all; SPLITS a comma list to sweep)
 #   emutrace:WL:RANKS     the same under --kernel-trace
 #   kb8:ARGS              tools/probe/kbench8.py ARGS (commas kept, '+' = space)
+#   kb8@NAME:ARGS         the same on an ablated copy (tools/probe/ablate.py NAME)
 set -o pipefail
 mkdir -p gpurun_out
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -86,9 +87,12 @@ run_step() {
      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "gpurun_out/emutrace_$a" -o run -- \
        python3 tools/ring_emulate.py --workload "$a" --ranks "${b:-8}" --steps 3 \
        > "gpurun_out/emutrace_$a.log" 2>&1) || fail "$spec" $? ;;
-  kb8)
-    local args=${spec#kb8:}
-    timeout -k 10 300 python -u tools/probe/kbench8.py ${args//+/ } >> gpurun_out/kb8.log 2>&1 \
+  kb8|kb8@*)
+    # kb8@NAME:ARGS times the ablated copy tools/probe/abl/libkbench8_NAME.so
+    local args=${spec#*:} so=""
+    [ "${kind#kb8@}" != "$kind" ] && so="tools/probe/abl/libkbench8_${kind#kb8@}.so"
+    echo "== $spec" >> gpurun_out/kb8.log
+    KB8_SO=$so timeout -k 10 300 python -u tools/probe/kbench8.py ${args//+/ } >> gpurun_out/kb8.log 2>&1 \
       || { rc=$?; tail -20 gpurun_out/kb8.log; fail "$spec" $rc; }
     grep '^{' gpurun_out/kb8.log | tail -40 ;;
   *) echo "unknown step $spec"; exit 2 ;;

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Ablated copies of k_dist_topk_i8 for kbench8 (diagnostic; the product
+source carries no hooks).  Each variant is the product file with textual
+patches applied, compiled into tools/probe/abl/libkbench8_<name>.so; time it
+with  KB8_SO=tools/probe/abl/libkbench8_<name>.so python tools/probe/kbench8.py
+
+  noepi        the per-tile epilogue replaced by an XOR sink of the
+               accumulators (kept live; no survivor code compiled in)
+  noepi_nodma  ... and no LDS-DMA staging (fragments read stale LDS)
+  noepi_nodma_nobar  ... and no per-chunk barrier
+  nodma        epilogue kept, staging removed (garbage keys: timing only)
+  noepi_halfdma  one of each wave's two pieces a chunk (timing only)
+  noepi_nowait   pieces issued, never waited for (racy: timing only)
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "..", "..", "mpi-knn_amd", "csrc", "knn_i8.hip")
+
+SINK = ("""            { int sk = 0;
+#pragma unroll
+              for (int bb = 0; bb < MB; bb++)
+#pragma unroll
+                for (int i = 0; i < 16; i++) sk ^= acc[bb][i];
+              if (sk == 0x12345678) part_T[0] = 1.0; }
+""")
+
+
+def patch(s, name):
+    if "noepi" in name:
+        old = "            epilogue(t, acc, x);\n"
+        assert old in s
+        s = s.replace(old, SINK)
+    if "nodma" in name:
+        for old in ("        if constexpr (PW == 4) bglds16x4(i8_rsrc(s_row + s_coff), voff[0], voff[1], voff[2], voff[3], dst);\n"
+                    "        else bglds16x2(i8_rsrc(s_row + s_coff), voff[0], voff[1], dst);\n",):
+            assert old in s
+            s = s.replace(old, "        (void)dst;\n")
+    if "halfdma" in name:
+        old = "        else bglds16x2(i8_rsrc(s_row + s_coff), voff[0], voff[1], dst);\n"
+        assert old in s
+        s = s.replace(old, "        else bglds16(i8_rsrc(s_row + s_coff), voff[0], dst);\n")
+        old = 'asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (NST - 3)) : "memory");'
+        assert old in s
+        s = s.replace(old, 'asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PW / 2) * (NST - 3)) : "memory");')
+    if "nowait" in name:
+        old = 'asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (NST - 3)) : "memory");'
+        assert old in s
+        s = s.replace(old, '')
+    if "nobar" in name:
+        old = "                            __builtin_amdgcn_s_barrier();   // B(x + 1)\n"
+        assert old in s
+        s = s.replace(old, "")
+    return s
+
+
+def main():
+    names = sys.argv[1:] or ["noepi", "noepi_nodma", "noepi_nodma_nobar", "nodma"]
+    out = os.path.join(HERE, "abl")
+    os.makedirs(out, exist_ok=True)
+    src = open(SRC).read()
+    for name in names:
+        f = os.path.join(out, "knn_i8_%s.hip" % name)
+        open(f, "w").write(patch(src, name))
+        so = os.path.join(out, "libkbench8_%s.so" % name)
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-I" + os.path.join(HERE, "..", "..", "include"),
+               "-I" + os.path.join(HERE, "..", "..", "mpi-knn_amd", "csrc"),
+               "-mllvm", "-disable-promote-alloca-to-lds", '-DKB8_SRC="%s"' % f, "-o", so,
+               os.path.join(HERE, "kbench8.hip")]
+        subprocess.check_call(cmd)
+        print(so)
+
+
+if __name__ == "__main__":
+    main()

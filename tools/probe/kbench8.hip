@@ -4,7 +4,12 @@
 // HIP events; the bounds array is reset to +inf before every launch, kept
 // from the previous launch (converged), or taken as given (preset by the
 // driver).  Driven by tools/probe/kbench8.py (data from the real engine).
-#include "../../mpi-knn_amd/csrc/knn_i8.hip"
+// KB8_SRC: the kernel source (the product file, or an ablated copy made by
+// tools/probe/ablate.py)
+#ifndef KB8_SRC
+#define KB8_SRC "../../mpi-knn_amd/csrc/knn_i8.hip"
+#endif
+#include KB8_SRC
 #include <string.h>
 
 __global__ void kb8_fill_inf(double *p, int n)
