@@ -2,7 +2,7 @@
  * knn_engine.c -- host side of libknn (C, HIP runtime API).
  *
  * Owns device buffers and sequences the kernels of knn_kernels.hip:
- *   knn_block_pack  -> k_pack + k_norms      (blk:100-109 packing)
+ *   knn_block_pack  -> k_pack_col / k_pack_row (blk:100-109 packing)
  *   knn_ctx_step    -> k_dist_topk + k_merge (one ring step, blk:217-242)
  *   knn_ctx_end     -> k_finalize            (+ rescan pass when needed)
  * and implements the one-call knn_search() of include/knn.h on top.

@@ -4,8 +4,9 @@
 // knn-serial.c:72-93 (and its per-block copies mpi-knn-parallel_blocking.c:
 // 155-181, 217-242).  Re-designed for MI355X:
 //
-//   k_pack       column/row-major fp64 -> padded row-major block + norms +
-//                meta (replaces blk:100-109's packing).
+//   k_pack_col / k_pack_row   column/row-major fp64/fp32 -> padded
+//                row-major block + norms + meta in one pass (replaces
+//                blk:100-109's packing).
 //   k_dist_topk  fused fp64-MFMA contraction G = C.Q^T (v_mfma_f64_16x16x4)
 //                with d^2 = |q|^2 + |c|^2 - 2G and a per-lane register top-k
 //                (insertion network) behind a shared threshold.  One
@@ -168,56 +169,18 @@ __device__ __forceinline__ double knn_cert_E(int n, double qn, double maxnorm)
 }
 
 // ---------------------------------------------------------------------------
-// k_pack: src (S = fp64 or fp32; col-major, ld >= rows | row-major, ld >= n)
-// -> padded row-major block of T.  64x64 tiles through LDS so both sides
-// stay coalesced.
+// Packing (blk:100-109): src (S = fp64 or fp32; col-major, ld >= rows |
+// row-major, ld >= n) -> padded row-major block of T, the squared norms
+// (fp64 accumulate, stored as T) and the meta (max|x|, max norm,
+// non-integer, non-finite, max(x)+, max(-x)+), in ONE pass over the source
+// (the norms are taken from the stored T values).  Per workgroup the meta
+// is reduced, then one atomicMax per word (non-negative doubles order like
+// their bits; the caller zeroes the meta).
 // ---------------------------------------------------------------------------
-template <typename T, typename S>
-__global__ __launch_bounds__(256) void k_pack(T *__restrict__ blk, size_t rows, size_t rows_pad,
-                                              int n, int n_pad, const S *__restrict__ src,
-                                              size_t ld, int layout)
-{
-    __shared__ T tile[64][65];
-    const size_t i0 = (size_t)blockIdx.x * 64;
-    const int j0 = blockIdx.y * 64;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    if (layout == KNN_COLMAJOR) {
-        for (int jj = ty; jj < 64; jj += 4) {
-            size_t i = i0 + tx;
-            int j = j0 + jj;
-            tile[jj][tx] = (i < rows && j < n) ? (T)src[i + (size_t)j * ld] : (T)0;
-        }
-    } else {
-        for (int ii = ty; ii < 64; ii += 4) {
-            size_t i = i0 + ii;
-            int j = j0 + tx;
-            tile[tx][ii] = (i < rows && j < n) ? (T)src[i * ld + j] : (T)0;
-        }
-    }
-    __syncthreads();
-    for (int ii = ty; ii < 64; ii += 4) {
-        size_t i = i0 + ii;
-        int j = j0 + tx;
-        if (i < rows_pad && j < n_pad) blk[i * n_pad + j] = tile[tx][ii];
-    }
-}
-
-// One wave per row: squared norm (accumulated in fp64, stored as T) + meta
-// (max|x|, max norm, non-integer, non-finite, max(x)+, max(-x)+).
-// Block-reduced, then one atomicMax per block and word.
-template <typename T>
-__global__ __launch_bounds__(256) void k_norms(T *__restrict__ blk, size_t rows, size_t rows_pad,
-                                               int n, int n_pad)
-{
-    T *norms = blk + rows_pad * (size_t)n_pad;
-    double *meta = (double *)(norms + rows_pad);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    double mabs = 0.0, mnorm = 0.0, nonint = 0.0, nonfin = 0.0, mpos = 0.0, mneg = 0.0;
-    // 16-byte loads (rows are whole 128-byte chunks, zero past n), four in
-    // flight a lane: the pass is bound by load latency, not by its ALU work
-    typedef typename std::conditional<sizeof(T) == 8, dbl2, flt4>::type vec_t;
-    constexpr int V = 16 / (int)sizeof(T);
-    auto acc = [&](double v, double &s) {
+struct knn_meta_acc {
+    double mabs = 0.0, nonint = 0.0, nonfin = 0.0, mpos = 0.0, mneg = 0.0;
+    __device__ __forceinline__ void add(double v, double &s)
+    {
         s = fma(v, v, s);
         if (!__builtin_isfinite(v)) nonfin = 1.0;
         else {
@@ -227,40 +190,18 @@ __global__ __launch_bounds__(256) void k_norms(T *__restrict__ blk, size_t rows,
             mneg = -v > mneg ? -v : mneg;
             if (v != rint(v)) nonint = 1.0;
         }
-    };
-    for (size_t i = (size_t)blockIdx.x * 4 + wave; i < rows_pad; i += (size_t)gridDim.x * 4) {
-        const vec_t *x = (const vec_t *)(blk + i * n_pad);
-        double s = 0.0;
-        if (i < rows) {
-            const int nv = n_pad / V;              // whole vectors a row
-            for (int j0 = lane; j0 < nv; j0 += 4 * 64) {
-                vec_t w[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int j = j0 + 64 * u;
-                    if (j < nv) w[u] = x[j];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int j = j0 + 64 * u;
-                    if (j < nv) {
-#pragma unroll
-                        for (int e = 0; e < V; e++)
-                            if (j * V + e < n) acc((double)w[u][e], s);
-                    }
-                }
-            }
-        }
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-        if (lane == 0) norms[i] = (T)s;
-        if (s == s) mnorm = s > mnorm ? s : mnorm;
-        else nonfin = 1.0;
     }
-    double w[6] = {mabs, mnorm, nonint, nonfin, mpos, mneg};
+};
+
+// workgroup reduction of the 6 meta words (256 threads) + atomicMax
+__device__ __forceinline__ void knn_meta_flush(const knn_meta_acc &a, double mnorm, double *meta)
+{
+    __shared__ double red[4][6];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double w[6] = {a.mabs, mnorm, a.nonint, a.nonfin, a.mpos, a.mneg};
 #pragma unroll
     for (int q = 0; q < 6; q++)
         for (int off = 32; off > 0; off >>= 1) w[q] = fmax(w[q], __shfl_xor(w[q], off));
-    __shared__ double red[4][6];
     if (lane == 0) {
 #pragma unroll
         for (int q = 0; q < 6; q++) red[wave][q] = w[q];
@@ -269,11 +210,81 @@ __global__ __launch_bounds__(256) void k_norms(T *__restrict__ blk, size_t rows,
     if (threadIdx.x < 6) {
         double v = fmax(fmax(red[0][threadIdx.x], red[1][threadIdx.x]),
                         fmax(red[2][threadIdx.x], red[3][threadIdx.x]));
-        if (!(v >= 0.0)) v = __builtin_inf();  // NaN norm -> treat as overflow
-        // non-negative doubles order like their bit patterns
-        atomicMax((unsigned long long *)&meta[threadIdx.x],
-                  (unsigned long long)__double_as_longlong(v));
+        if (!(v >= 0.0)) v = __builtin_inf();   // NaN norm -> treat as overflow
+        atomicMax((unsigned long long *)&meta[threadIdx.x], (unsigned long long)__double_as_longlong(v));
     }
+}
+
+// Column-major source (the .mat layout): a workgroup owns 64 rows and walks
+// the columns in 64 x 64 tiles through LDS (reads: 64 consecutive rows of a
+// column, 512 B; writes: 64 consecutive features of a row).  Thread (ty,
+// tx) accumulates row tx's squared terms over columns = ty mod 4; the four
+// partials are summed at the end (a fixed order).
+template <typename T, typename S>
+__global__ __launch_bounds__(256) void k_pack_col(T *__restrict__ blk, size_t rows, size_t rows_pad,
+                                                  int n, int n_pad, const S *__restrict__ src, size_t ld)
+{
+    __shared__ T tile[64][65];
+    __shared__ double part[4][64];
+    T *norms = blk + rows_pad * (size_t)n_pad;
+    double *meta = (double *)(norms + rows_pad);
+    const size_t i0 = (size_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const size_t i = i0 + tx;
+    knn_meta_acc ma;
+    double s = 0.0;
+    for (int j0 = 0; j0 < n_pad; j0 += 64) {
+#pragma unroll 4
+        for (int jj = ty; jj < 64; jj += 4) {
+            const int j = j0 + jj;
+            const T v = (i < rows && j < n) ? (T)src[i + (size_t)j * ld] : (T)0;
+            tile[jj][tx] = v;
+            ma.add((double)v, s);
+        }
+        __syncthreads();
+        const int j = j0 + tx;
+#pragma unroll 4
+        for (int ii = ty; ii < 64; ii += 4)
+            if (i0 + ii < rows_pad && j < n_pad) blk[(i0 + ii) * n_pad + j] = tile[tx][ii];
+        __syncthreads();
+    }
+    part[ty][tx] = s;
+    __syncthreads();
+    double mnorm = 0.0;
+    if (ty == 0 && i < rows_pad) {
+        const double nr = (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]);
+        norms[i] = (T)nr;
+        if (nr == nr) mnorm = nr;
+        else ma.nonfin = 1.0;
+    }
+    knn_meta_flush(ma, mnorm, meta);
+}
+
+// Row-major source: one wave per row (lane-strided features, butterfly sum).
+template <typename T, typename S>
+__global__ __launch_bounds__(256) void k_pack_row(T *__restrict__ blk, size_t rows, size_t rows_pad,
+                                                  int n, int n_pad, const S *__restrict__ src, size_t ld)
+{
+    T *norms = blk + rows_pad * (size_t)n_pad;
+    double *meta = (double *)(norms + rows_pad);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    knn_meta_acc ma;
+    double mnorm = 0.0;
+    for (size_t i = (size_t)blockIdx.x * 4 + wave; i < rows_pad; i += (size_t)gridDim.x * 4) {
+        double s = 0.0;
+        const S *x = src + i * ld;
+        T *o = blk + i * (size_t)n_pad;
+        for (int j = lane; j < n_pad; j += 64) {
+            const T v = (i < rows && j < n) ? (T)x[j] : (T)0;
+            o[j] = v;
+            ma.add((double)v, s);
+        }
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+        if (lane == 0) norms[i] = (T)s;
+        if (s == s) mnorm = s > mnorm ? s : mnorm;
+        else ma.nonfin = 1.0;
+    }
+    knn_meta_flush(ma, mnorm, meta);
 }
 
 // ---------------------------------------------------------------------------
@@ -1575,13 +1586,14 @@ static int launch_pack(T *blk, size_t cap, size_t rows, size_t n, const S *src, 
     double *meta = (double *)(blk + rp * np + rp);
     if (hipMemsetAsync(meta, 0, KNN_META_DOUBLES * sizeof(double), s) != hipSuccess)
         return KNN_ERR_HIP;
-    dim3 grid((unsigned)((rp + 63) / 64), (unsigned)((np + 63) / 64));
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack<T, S>), grid, dim3(256), 0, s, blk, rows, rp, (int)n,
-                       (int)np, src, ld, layout);
-    unsigned nb = (unsigned)((rp / 4) < 4096 ? (rp / 4) : 4096);
-    if (nb == 0) nb = 1;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_norms<T>), dim3(nb), dim3(256), 0, s, blk, rows, rp, (int)n,
-                       (int)np);
+    if (layout == KNN_COLMAJOR) {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack_col<T, S>), dim3((unsigned)((rp + 63) / 64)), dim3(256), 0, s,
+                           blk, rows, rp, (int)n, (int)np, src, ld);
+    } else {
+        const unsigned nb = (unsigned)((rp + 3) / 4 < 8192 ? (rp + 3) / 4 : 8192);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack_row<T, S>), dim3(nb), dim3(256), 0, s, blk, rows, rp,
+                           (int)n, (int)np, src, ld);
+    }
     return hip_status();
 }
 
