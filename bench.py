@@ -235,8 +235,13 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         pass
     # the MFMA the contraction ran on: fp32 searches on exactly representable
     # 8-bit-style integer data contract on fp16 MFMA (include/knn.h)
+    split = engine.ctx.split()
     peak = {64: FP64_MFMA_PEAK_TFLOPS, 32: FP32_MFMA_PEAK_TFLOPS,
             16: FP16_MFMA_PEAK_TFLOPS, 8: I8_MFMA_PEAK_TOPS}[cbits]
+    if split:
+        # split fp16 filter: 3 fp16 MFMAs (hi.hi, hi.lo, lo.hi) per
+        # algorithmic multiply-add, so its roofline is a third of fp16's
+        peak = FP16_MFMA_PEAK_TFLOPS / 3.0
     dtype_peak = FP64_MFMA_PEAK_TFLOPS if dtype == "f64" else FP32_MFMA_PEAK_TFLOPS
     roofline = {
         "kernel": "k_dist_topk_i8" if cbits == 8 else "k_dist_topk",
@@ -244,7 +249,9 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         "achieved": achieved,
         "peak": peak,
         "unit": "TFLOP/s",
-        "mfma_input": {64: "f64", 32: "f32", 16: "f16 (exact on this data)",
+        "mfma_input": "f16 split x S = hi + lo (3 MFMAs a product; exact after the fp64 re-rank and "
+                      "certificate)" if split else
+                      {64: "f64", 32: "f32", 16: "f16 (exact on this data)",
                        8: "i8 (exact on this data: int32 dot products)"}[cbits],
         "frac": (achieved / peak) if achieved else None,
         "frac_basis": "achieved = algorithmic FLOP / distance-kernel busy time from HIP events on the "
@@ -255,6 +262,7 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         # (BASELINE's "% of fp64 MFMA peak" wording) is an equivalent, > 1 here
         "frac_of_dtype_peak": (achieved / dtype_peak) if (achieved and cbits >= 32) else None,
         "dtype_peak_equiv": (achieved / dtype_peak) if (achieved and cbits < 32) else None,
+        "filter": "split-f16" if split else None,
         "traffic": traffic,
         "traffic_source": "rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE of the same workload at P = 1 "
                           "(profiles/pmc_traffic.json; not measured inside this run)" if traffic else None,

@@ -22,9 +22,10 @@
  *
  * Environment switches read by the library (none changes a result; each
  * selects among exact code paths, for tests and diagnosis):
- *   KNN_NO_I8=1 / KNN_NO_H16=1 / KNN_NO_SHADOW=1
+ *   KNN_NO_I8=1 / KNN_NO_H16=1 / KNN_NO_SHADOW=1 / KNN_NO_SPLIT=1
  *                         disable the int8 / fp16 contraction / fp16 shadow
- *                         rows (the next exact contraction in line runs)
+ *                         rows / split fp16 filter (the next exact
+ *                         contraction in line runs)
  *   KNN_I8_KL=17          17-entry int8 lane lists instead of 12
  *   KNN_SPLITS=s          corpus splits per launch instead of the model's
  *   KNN_NO_FUSE=1         fold received byte blocks one launch each
@@ -317,6 +318,13 @@ KNN_API int knn_ctx_info(const knn_ctx_t *ctx, int *mode, int *splits);
  * exact int32 dot products; KNN_NO_I8=1 disables it).  Set by
  * knn_ctx_begin.  0 for a NULL context. */
 KNN_API int knn_ctx_contraction_bits(const knn_ctx_t *ctx);
+/* 1 when the current search filters with the split fp16 contraction: fp32
+ * blocks in GEMM mode (non-integer data), each value scaled by a power of
+ * two S and split as S x = hi + lo in fp16, hi.hi + hi.lo + lo.hi on fp16
+ * MFMA (fp32 accumulate); the candidates are re-ranked by the exact fp64 S
+ * and certified with that filter's error bound (knn_cert_E), so results are
+ * those of the fp32 MFMA filter, bit for bit.  KNN_NO_SPLIT=1 disables it. */
+KNN_API int knn_ctx_split(const knn_ctx_t *ctx);
 
 /* Kernel timing with HIP events on the launch streams (the timers of
  * serial:70-98 at kernel granularity).  enable = 1 starts recording and

@@ -43,6 +43,10 @@ struct knn_ctx {
     size_t qsh_bytes, csh_bytes;
     void *qs8, *cs8[KNN_PSETS];   /* byte blocks: the queries, converted corpus blocks */
     size_t qs8_bytes;
+    int split;          /* this search filters with the split fp16 contraction (fp32 GEMM mode) */
+    float sscale;       /* its power-of-two pre-scale S */
+    void *qsp, *csp[KNN_PSETS];   /* split shadow rows: the queries, converted corpus blocks */
+    size_t qsp_bytes, csp_bytes;
     int lpq, klx;       /* partial lists of the active kernel: lpq per query and split, klx long */
     int cus;
     /* per-step partial lists of k_dist_topk, KNN_PSETS sets used in turn
@@ -246,6 +250,8 @@ static void ctx_free_buffers(knn_ctx_t *c)
     for (int b = 0; b < KNN_PSETS; b++) hipFree(c->csh[b]);
     hipFree(c->qs8);
     for (int b = 0; b < KNN_PSETS; b++) hipFree(c->cs8[b]);
+    hipFree(c->qsp);
+    for (int b = 0; b < KNN_PSETS; b++) hipFree(c->csp[b]);
     if (c->ev_in) hipEventDestroy(c->ev_in);
     hipFree(c->qthr);
     hipFree(c->st_d);
@@ -409,8 +415,10 @@ int knn_ctx_contraction_bits(const knn_ctx_t *c)
 {
     if (!c) return 0;
     if (c->i8) return 8;
-    return c->h16 ? 16 : (c->dtype == KNN_F64 ? 64 : 32);
+    return (c->h16 || c->split) ? 16 : (c->dtype == KNN_F64 ? 64 : 32);
 }
+
+int knn_ctx_split(const knn_ctx_t *c) { return c ? c->split : 0; }
 
 int knn_ctx_info(const knn_ctx_t *c, int *mode, int *splits)
 {
@@ -462,6 +470,26 @@ static int env_on(const char *name)
     return e && e[0] == '1';
 }
 
+/* The split fp16 filter serves fp32 searches in GEMM mode (knn_mode<float>:
+ * finite, norms below 1e37, not the exact-integer INT mode, whose filter
+ * must be exact).  Returns the pre-scale S = 2^(14 - e) with maxabs in
+ * [2^(e-1), 2^e), so maxabs S in [2^13, 2^14) fits fp16 with room, or 0
+ * when the filter does not apply (S^2 must stay well inside fp32, and the
+ * epilogue's -2 / S^2 too). */
+static float knn_split_scale(const double *meta, size_t n, int dtype)
+{
+    if (dtype != KNN_F32 || meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e37)) return 0.f;
+    const double mx = meta[KNN_META_MAXABS];
+    const double rg = meta[KNN_META_MAXPOS] + meta[KNN_META_MAXNEG];
+    if (meta[KNN_META_NONINT] == 0.0 && (double)n * mx * mx <= 8388608.0 && (double)n * rg * rg <= 16777216.0)
+        return 0.f;   /* INT mode */
+    if (!(mx > 0.0)) return 0.f;
+    int e = 0;
+    (void)frexp(mx, &e);
+    if (e < -40 || e > 40) return 0.f;
+    return (float)ldexp(1.0, 14 - e);
+}
+
 int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_base,
                        const double *d_meta, const double *h_meta, void *stream)
 {
@@ -485,8 +513,10 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
      * KNN_NO_H16=1 disable them).  A caller that holds the host copy of
      * the meta (the ring drivers, after their all-reduce) passes it; else
      * one 64-byte read. */
-    const int no_i8 = env_on("KNN_NO_I8"), no_h16 = env_on("KNN_NO_H16");
-    if (!(no_i8 && no_h16)) {
+    const int no_i8 = env_on("KNN_NO_I8"), no_h16 = env_on("KNN_NO_H16"), no_split = env_on("KNN_NO_SPLIT");
+    c->split = 0;
+    c->sscale = 0.f;
+    if (!(no_i8 && no_h16 && no_split)) {
         double hm[KNN_META_DOUBLES];
         if (!h_meta) {
             HIPCHK(hipMemcpyAsync(hm, d_meta, sizeof(hm), hipMemcpyDeviceToHost, (hipStream_t)stream));
@@ -495,6 +525,10 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
         }
         c->i8 = !no_i8 && knn_i8_exact(h_meta, c->n, c->dtype);
         c->h16 = !c->i8 && !no_h16 && knn_h16_exact(h_meta, c->n, c->dtype);
+        if (!c->i8 && !c->h16 && !no_split) {
+            c->sscale = knn_split_scale(h_meta, c->n, c->dtype);
+            c->split = c->sscale > 0.f;
+        }
     }
     c->lpq = c->i8 ? knn_i8_lpq(c->kp) : 4;
     /* int8 lane lists: 12 entries (k <= 32), 17 on request (KNN_I8_KL=17) */
@@ -515,6 +549,17 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
             c->qs8_bytes = need;
         }
         RCHK(knn_launch_shadow8(c->qs8, d_qblock, c->dtype, c->q_rows_pad, c->n, d_meta, stream));
+    } else if (c->split) {
+        const size_t need = c->q_rows_pad * knn_split_rs(c->n);
+        if (need > c->qsp_bytes) {
+            HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+            hipFree(c->qsp);
+            c->qsp = NULL;
+            c->qsp_bytes = 0;
+            if (hipMalloc(&c->qsp, need) != hipSuccess) return KNN_ERR_NOMEM;
+            c->qsp_bytes = need;
+        }
+        RCHK(knn_launch_shadow_split(c->qsp, d_qblock, c->q_rows_pad, c->n, c->sscale, stream));
     } else if (c->shadow) {
         const size_t need = c->q_rows_pad * knn_round_up(c->n, 64) * 2;
         if (need > c->qsh_bytes) {
@@ -726,7 +771,7 @@ static int launch_merge_sets(knn_ctx_t *c, int set, int nsets, int nsplit_total,
     RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
                           nsplit_total, c->lpq, c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x,
                           c->st_i, c->st_T, c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n,
-                          c->meta, c->qthr, c->ms));
+                          c->meta, c->qthr, c->split, c->ms));
     c->merged = 1;
     for (int x = 0; x < nsets; x++) HIPCHK(hipEventRecord(c->ev_m[(set + x) % KNN_PSETS], c->ms));
     return KNN_OK;
@@ -847,6 +892,24 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
                                     c->meta, ds));
             csh = c->cs8[set];
         }
+    } else if (c->split) {
+        if (d_cblock == c->qblk && knn_rows_pad(c->block_cap) == c->q_rows_pad) {
+            csh = c->qsp;   /* the query block itself (P = 1) */
+        } else {
+            const size_t need = knn_rows_pad(c->block_cap) * knn_split_rs(c->n);
+            if (need > c->csp_bytes) {
+                /* the sets may still be read by earlier steps' kernels */
+                HIPCHK(hipDeviceSynchronize());
+                for (int b = 0; b < KNN_PSETS; b++) {
+                    hipFree(c->csp[b]);
+                    c->csp[b] = NULL;
+                }
+                c->csp_bytes = need;
+            }
+            if (!c->csp[set] && hipMalloc(&c->csp[set], c->csp_bytes) != hipSuccess) return KNN_ERR_NOMEM;
+            RCHK(knn_launch_shadow_split(c->csp[set], d_cblock, knn_rows_pad(nc), c->n, c->sscale, ds));
+            csh = c->csp[set];
+        }
     } else if (d_sblock) {
         cn_ptr = (const char *)d_sblock + knn_shadow_norm_offset(c->block_cap, c->n);
     } else if (c->shadow && d_cblock == c->qblk && knn_rows_pad(nc) <= c->q_rows_pad) {
@@ -880,10 +943,10 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
         RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq,
                                   cblk, knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta,
                                   nsplit, c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad,
-                                  c->qthr, c->qsh, csh, cn_ptr,
+                                  c->qthr, c->split ? c->qsp : c->qsh, csh, cn_ptr,
                                   (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0) |
-                                      (c->shadow ? KNN_DIST_SHADOW : 0),
-                                  ds));
+                                      (c->shadow ? KNN_DIST_SHADOW : 0) | (c->split ? KNN_DIST_SPLIT : 0),
+                                  c->split ? (float)(-2.0 / ((double)c->sscale * c->sscale)) : -2.f, ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
     HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
     HIPCHK(hipEventRecord(c->ev_ds[set], ds));
@@ -970,7 +1033,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
                              (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
                              c->fail_list, c->mode_dev, c->fbound, env_on("KNN_FORCE_RESCAN"),
-                             stream));
+                             c->split, stream));
     int host[2];
     HIPCHK(hipMemcpyAsync(&host[0], c->fail_count, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&host[1], c->mode_dev, sizeof(int), hipMemcpyDeviceToHost, s));

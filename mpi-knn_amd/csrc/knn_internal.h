@@ -112,14 +112,21 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
                          int n, const double *meta, int nsplit,
                          double *part_d, int *part_i, double *part_T, int nq_pad,
                          double *qthr, const void *qsh, const void *csh, const void *cn_ptr,
-                         int flags, void *stream);
+                         int flags, float m2s, void *stream);
 /* knn_launch_dist_topk flags */
 #define KNN_DIST_XORD   1  /* XCD-grouped workgroup order                        */
 #define KNN_DIST_H16    2  /* fp16 MFMA contraction (exact data only)             */
 #define KNN_DIST_SHADOW 4  /* with H16: stage the fp16 shadow rows qsh / csh      */
+#define KNN_DIST_SPLIT  8  /* fp32 blocks: split fp16 filter on the split shadow rows
+                              qsh / csh (knn_launch_shadow_split); m2s = -2 / S^2   */
 /* fp16 shadow rows (round_up(n, 64) halves a row) of a packed block */
 int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
+/* split fp16 shadow rows of an fp32 block: per 32 features 32 halves hi =
+ * RN16(S x), then 32 halves lo = RN16(S x - hi); rows of round_up(n, 32) * 4
+ * bytes; S a power of two (knn_engine.c: maxabs S in [2^13, 2^14)) */
+static inline size_t knn_split_rs(size_t n) { return knn_round_up(n ? n : 1, 32) * 4; }
+int knn_launch_shadow_split(void *dst, const void *blk, size_t rows_pad, size_t n, float S, void *stream);
 /* knn_i8.hip: element block -> byte block (meta = the reduced meta) and the
  * int8 distance + top-k kernel (partial lists [split][query][2][kl]) */
 int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,
@@ -133,12 +140,12 @@ int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *
                      int first_step,
                      double *st_d, double *st_x, int *st_i, double *st_T, const void *qblk,
                      size_t q_rows_pad, const void *cblk, size_t c_base, int nc, int n,
-                     const double *meta, double *qthr, void *stream);
+                     const double *meta, double *qthr, int filt, void *stream);
 int knn_launch_finalize(int dtype, int kp, const double *st_d, const double *st_x, const int *st_i,
                         const double *st_T, const void *qblk, size_t q_rows_pad,
                         int nq, int n, int k, const double *meta,
                         knn_neighbour_t *out, int *fail_count, int *fail_list,
-                        int *mode_out, double *fbound, int force_fail, void *stream);
+                        int *mode_out, double *fbound, int force_fail, int filt, void *stream);
 int knn_launch_rescan_init(int kp, double *rs_d, int *rs_i, int nfail, void *stream);
 int knn_launch_rescan_step(int dtype, int kp, const int *fail_list, int nfail,
                            const double *fbound, const void *qblk, const void *cblk,

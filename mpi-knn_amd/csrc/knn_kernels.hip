@@ -159,11 +159,31 @@ __device__ __forceinline__ double knn_exact_sq_v(const T *__restrict__ a, const 
 //   two final roundings 4u (|q|^2+|c|^2), times (1 + 2(n+4)u) for the
 //   second-order terms; the reference's fp64 S: 4(n+2) 2^-53 (|q|^2+|c|^2).
 //   fp64 filter: both at u = 2^-53, 8(n+4)u (|q|^2+|c|^2).
+//   split fp16 filter (fp32 blocks, knn_shadow_split): each value scaled by
+//   S = 2^e (maxabs S in [2^13, 2^14)) and split x S = hi + lo in fp16;
+//   hi.hi + hi.lo + lo.hi on v_mfma_f32_16x16x32_f16.  Per element
+//   |xS - hi - lo| <= 2^-22 |xS| + 2^-25 and the dropped lo.lo <=
+//   2^-22 |q_j c_j| (+ subnormal terms): 3 2^-22 sum|q_j c_j|, 12u qc for d^2.
+//   fp16 products are exact in fp32; the accumulator sums n hi.hi products
+//   and n/32 per-chunk cross-term sums (any order, fp32: <= 1.05 n u
+//   sum|terms|), 1.05 n u qc for d^2; norms, qn + cn and the final fma 4u
+//   qc.  With a 20% margin on the accumulation (the MFMA's internal order
+//   is not specified; its precision is at least fp32): ((1.25 n + 24) u +
+//   4 (n+4) 2^-53) qc.  Subnormal fp16 halves may be flushed by the MFMA:
+//   then up to 2^-14 / S <= 2^-27 maxabs is lost per element, the absolute
+//   part 2^-26 maxabs sqrt(n) (|q| + |c|).  The fp32 filter's is ~ (n + 4)
+//   u qc.
 template <typename TE>
-__device__ __forceinline__ double knn_cert_E(int n, double qn, double maxnorm)
+__device__ __forceinline__ double knn_cert_E(int n, double qn, double maxnorm, int split = 0,
+                                             double maxabs = 0.0)
 {
     const double u = KT<TE>::U;
     const double nn = (double)n + 4.0, qc = qn + maxnorm;
+    if (split) {
+        const double ul = 5.9604644775390625e-08;   // 2^-24
+        return ((1.25 * n + 24.0) * ul + 4.0 * nn * 1.1102230246251565e-16) * qc * (1.0 + 1e-6) +
+               1.4901161193847656e-08 * maxabs * sqrt((double)n) * (sqrt(qn) + sqrt(maxnorm));
+    }
     if constexpr (sizeof(TE) == 8) return 8.0 * nn * u * qc;
     else return nn * qc * (u * (1.0 + 2.0 * nn * u) + 4.0 * 1.1102230246251565e-16);
 }
@@ -350,16 +370,19 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const T *__restrict__ cblk, const T *__restrict__ cnorm, size_t c_base, int nc,
     int n, int n_pad, int ntiles, int nsplit, int nqb, const double *__restrict__ meta,
     double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T,
-    int nq_pad, unsigned long long *__restrict__ qthr, int uj, int xord)
+    int nq_pad, unsigned long long *__restrict__ qthr, int uj, int xord, float m2s)
 {
     constexpr int NST = KNN_NST;
     // H16 2: qblk / cblk are fp16 shadow rows (k_shadow), n_pad their row
     // length; the norms stay in the element blocks
-    constexpr int RS = H16 == 2 ? 2 : (int)sizeof(T);   // bytes per staged element
+    // H16 3: split fp16 shadow rows (knn_shadow_split, 4 bytes a feature:
+    // per 32 features 32 hi halves then 32 lo halves), fp32 blocks only
+    static_assert(H16 != 3 || sizeof(T) == 4, "split fp16 filter: fp32 blocks");
+    constexpr int RS = H16 == 2 ? 2 : (H16 == 3 ? 4 : (int)sizeof(T));   // bytes per staged element
     constexpr int BK = 128 / RS;                      // features per 128-B chunk
     // fp64 H16 (knn_to_h4): the fp32 MFMA output layout, row 4g + r of a
     // 16-row m-tile in lane group g, register r, instead of fp64's g + 4r
-    constexpr bool H16D = H16 != 0 && sizeof(T) == 8;
+    constexpr bool H16D = H16 != 0 && H16 != 3 && sizeof(T) == 8;
     auto rowmap = [](int gg, int r) { return H16D ? 4 * gg + r : KT<T>::row(gg, r); };
     constexpr int ES = (int)sizeof(T);
     typedef typename KT<T>::acc_t acc_t;
@@ -544,7 +567,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             for (int m4 = 0; m4 < 4; m4++)
 #pragma unroll
                 for (int r = 0; r < 4; r++)
-                    A[4 * hh + m4][r] = fma((T)-2, A[4 * hh + m4][r], qn + cnr[m4][r]);
+                    A[4 * hh + m4][r] = fma(H16 == 3 ? (T)m2s : (T)-2, A[4 * hh + m4][r], qn + cnr[m4][r]);
         }
         T lanemin = A[0][0];
 #pragma unroll
@@ -722,6 +745,36 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                     glds1(0);
                     continue;
                 }
+                if constexpr (H16 == 3) {
+                    // split fp16: slot g of the chunk row holds the hi
+                    // halves of features 8g..8g+7 of the 32, slot 4+g their
+                    // lo halves; hi.hi + hi.lo + lo.hi (knn_cert_E, split)
+                    glds1(1);
+                    glds1(2);
+                    glds1(3);
+                    const knn_h8 qh = *(const LDS_AS knn_h8 *)(cs + 16384 + wave * 2048 + fslot);
+                    const knn_h8 ql = *(const LDS_AS knn_h8 *)(cs + 16384 + wave * 2048 + fslot1);
+#pragma unroll
+                    for (int mt = 0; mt < 8; mt++) {
+                        const knn_h8 ah = *(const LDS_AS knn_h8 *)(cs + mt * 2048 + fslot);
+                        const knn_h8 al = *(const LDS_AS knn_h8 *)(cs + mt * 2048 + fslot1);
+                        // the cross terms (~2^-11 of hi.hi) summed apart and
+                        // added once a chunk: the accumulator's rounding then
+                        // runs over n hi.hi products + n/32 small terms, not
+                        // 3n (knn_cert_E, split)
+                        flt4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ql, (flt4){0, 0, 0, 0}, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, qh, t, 0, 0, 0);
+                        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qh, acc[mt], 0, 0, 0);
+                        acc[mt] += t;
+                    }
+                    advance();
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    if constexpr (SELF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    glds1(0);
+                    continue;
+                }
                 if constexpr (H16 == 1 && H16D) {
                     // fp16 MFMA on converted fp64 fragments (knn_to_h4); the
                     // output is in the fp32 layout (rowmap)
@@ -884,7 +937,7 @@ __global__ __launch_bounds__(256) void k_merge(
     double *__restrict__ st_d, double *__restrict__ st_x, int *__restrict__ st_i,
     double *__restrict__ st_T, const TE *__restrict__ qblk, size_t qnorm_off,
     const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
-    const double *__restrict__ meta, int k, unsigned long long *__restrict__ qthr)
+    const double *__restrict__ meta, int k, unsigned long long *__restrict__ qthr, int filt)
 {
     // S lanes a query (64, or 32 when nl + 1 <= 32: two queries a wave, so
     // twice the independent argmin chains a SIMD interleaves -- the merge is
@@ -1101,7 +1154,9 @@ __global__ __launch_bounds__(256) void k_merge(
     // the top k: its S is skipped and marked +inf (k_finalize ignores it).
     double win = KNN_INF;
     if (mode == KNN_MODE_GEMM) {
-        const double E = qv ? knn_cert_E<TE>(n, (double)qblk[qnorm_off + q], meta[KNN_META_MAXNORM]) : 0.0;
+        const double E = qv ? knn_cert_E<TE>(n, (double)qblk[qnorm_off + q], meta[KNN_META_MAXNORM], filt,
+                                             meta[KNN_META_MAXABS])
+                            : 0.0;
         int z = 0;
 #pragma unroll
         for (int x = 0; x < NS; x++) z += __popcll(__ballot(sl + S * x < KP && sd[x] <= E) & segm);
@@ -1165,7 +1220,7 @@ __global__ __launch_bounds__(256) void k_finalize(
     const TE *__restrict__ qnorm, int nq, int n, int k,
     const double *__restrict__ meta, knn_neighbour_t *__restrict__ out,
     int *__restrict__ fail_count, int *__restrict__ fail_list, int *__restrict__ mode_out,
-    double *__restrict__ fbound, int force_fail)
+    double *__restrict__ fbound, int force_fail, int filt)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + wave;
@@ -1278,7 +1333,7 @@ __global__ __launch_bounds__(256) void k_finalize(
         }
         // E (knn_cert_E): |GEMM-form d^2 - exact S| plus the reference's
         // own rounding; T and Td are GEMM-form values
-        const double E = knn_cert_E<TE>(n, (double)qnorm[q], meta[KNN_META_MAXNORM]);
+        const double E = knn_cert_E<TE>(n, (double)qnorm[q], meta[KNN_META_MAXNORM], filt, meta[KNN_META_MAXABS]);
         ok = (Tb == KNN_INF) || ((Tb - E) > tau * (1.0 + 1.7763568394002505e-15));
     } else {
         ok = (Tb == KNN_INF);
@@ -1666,6 +1721,43 @@ extern "C" int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t r
     return hip_status();
 }
 
+// Split fp16 shadow rows (the H16 == 3 filter) of an fp32 block: per row and
+// 32-feature group, the 32 halves hi = RN16(S x) then the 32 halves lo =
+// RN16(S x - hi) (S x - hi is exact in fp32: Sterbenz); zero past n.  One
+// thread per 8 features: a 16-byte hi and a 16-byte lo store.
+__global__ __launch_bounds__(256) void k_shadow_split(char *__restrict__ dst, const float *__restrict__ src,
+                                                      size_t rows, int n, int nps, int npd, float S)
+{
+    const size_t per = (size_t)npd / 8, tot = rows * per;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < tot; i += (size_t)gridDim.x * 256) {
+        const size_t r = i / per;
+        const int j0 = (int)(i - r * per) * 8;
+        const float *row = src + r * (size_t)nps;
+        knn_h8 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const float x = j0 + e < n ? row[j0 + e] * S : 0.f;
+            const _Float16 h = (_Float16)x;
+            hi[e] = h;
+            lo[e] = (_Float16)(x - (float)h);
+        }
+        char *o = dst + r * (size_t)npd * 4 + (size_t)(j0 >> 5) * 128 + 2 * (j0 & 31);
+        *(knn_h8 *)o = hi;
+        *(knn_h8 *)(o + 64) = lo;
+    }
+}
+
+extern "C" int knn_launch_shadow_split(void *dst, const void *blk, size_t rows_pad, size_t n, float S,
+                                       void *stream)
+{
+    const int npd = (int)knn_round_up(n, 32), nps = (int)knn_n_pad_dt(n, KNN_F32);
+    const size_t tot = rows_pad * (size_t)npd / 8;
+    const unsigned grid = (unsigned)(tot / 256 + 1 < 8192 ? tot / 256 + 1 : 8192);
+    hipLaunchKernelGGL(k_shadow_split, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char *)dst,
+                       (const float *)blk, rows_pad, (int)n, nps, npd, S);
+    return hip_status();
+}
+
 extern "C" int knn_launch_wire(int unpack, void *dst, const void *src, int dtype, size_t cnt,
                                void *stream)
 {
@@ -1710,7 +1802,7 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
                             size_t c_rows_pad, size_t c_base, int nc, int n, const double *meta,
                             int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
                             double *qthr, int k, const void *qsh, const void *csh,
-                            const void *cn_ptr, int flags, hipStream_t s)
+                            const void *cn_ptr, int flags, float m2s, hipStream_t s)
 {
     const int xord = flags & 1;
     constexpr int dt = sizeof(T) == 8 ? KNN_F64 : KNN_F32;
@@ -1733,6 +1825,20 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     const T *cnorm = cn_ptr ? (const T *)cn_ptr : cblk + c_rows_pad * np;
     const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
     const dim3 grid((unsigned)(nqb_grid * nsplit));
+    if (flags & KNN_DIST_SPLIT) {
+        // split fp16 shadow rows (4 bytes a feature); m2s = -2 / S^2 undoes
+        // the scaling in the epilogue's fma (a power of two: exact)
+        if constexpr (sizeof(T) == 4) {
+            if (!qsh || !csh) return KNN_ERR_INVALID;
+            const int nps = (int)knn_round_up((size_t)n, 32);
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 3>), grid, dim3(512), 0, s,
+                               (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
+                               nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
+                               (unsigned long long *)qthr, uj, xord, m2s);
+            return hip_status();
+        }
+        return KNN_ERR_INVALID;
+    }
     if ((flags & KNN_DIST_SHADOW) && (flags & KNN_DIST_H16)) {
         if (!qsh || !csh) return KNN_ERR_INVALID;
         const int nps = (int)knn_round_up((size_t)n, 64);   // shadow row length (halves)
@@ -1744,12 +1850,12 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 2>), grid, dim3(512), 0, s,
                                (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
                                nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                               (unsigned long long *)qthr, uj, xord);
+                               (unsigned long long *)qthr, uj, xord, -2.f);
         else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 2>), grid, dim3(512), 0, s,
                                (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
                                nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                               (unsigned long long *)qthr, uj, xord);
+                               (unsigned long long *)qthr, uj, xord, -2.f);
         return hip_status();
     }
     {
@@ -1757,13 +1863,13 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 1>), grid, dim3(512), 0, s,
                                qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles, nsplit,
                                nqb, meta, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr,
-                               uj, xord);
+                               uj, xord, -2.f);
             return hip_status();
         }
     }
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP>), grid, dim3(512), 0, s, qblk, qnorm,
                        q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles, nsplit, nqb, meta, part_d,
-                       part_i, part_T, nq_pad, (unsigned long long *)qthr, uj, xord);
+                       part_i, part_T, nq_pad, (unsigned long long *)qthr, uj, xord, -2.f);
     return hip_status();
 }
 
@@ -1782,12 +1888,12 @@ extern "C" int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, 
                                     size_t c_base, int nc, int n, const double *meta, int nsplit,
                                     double *part_d, int *part_i, double *part_T, int nq_pad,
                                     double *qthr, const void *qsh, const void *csh,
-                                    const void *cn_ptr, int flags, void *stream)
+                                    const void *cn_ptr, int flags, float m2s, void *stream)
 {
 #define CALL(T, KL, KP)                                                                        \
     return launch_dist_topk<T, KL, KP>((const T *)qblk, q_rows_pad, q_base, nq, (const T *)cblk, \
                                        c_rows_pad, c_base, nc, n, meta, nsplit, part_d, part_i,  \
-                                       part_T, nq_pad, qthr, k, qsh, csh, cn_ptr, flags,          \
+                                       part_T, nq_pad, qthr, k, qsh, csh, cn_ptr, flags, m2s,     \
                                        (hipStream_t)stream)
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
@@ -1798,7 +1904,7 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
                                 int first_step, double *st_d, double *st_x, int *st_i,
                                 double *st_T, const void *qblk, size_t q_rows_pad,
                                 const void *cblk, size_t c_base, int nc, int n,
-                                const double *meta, double *qthr, void *stream)
+                                const double *meta, double *qthr, int filt, void *stream)
 {
     if (lpq < 1 || kl < 1 || lpq * nsplit + 1 > 64 || k <= 0 || k > kp) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
@@ -1814,22 +1920,22 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, 32, 32, 8>), grid, dim3(256), 0, s, part_d,  \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
                            st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
-                           np, meta, k, (unsigned long long *)qthr);                               \
+                           np, meta, k, (unsigned long long *)qthr, filt);                         \
     else if (pf && KP == 32)                                                                     \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, 32, 64, 8>), grid, dim3(256), 0, s, part_d,  \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
                            st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
-                           np, meta, k, (unsigned long long *)qthr);                               \
+                           np, meta, k, (unsigned long long *)qthr, filt);                         \
     else if (two)                                                                                \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP, 32>), grid, dim3(256), 0, s, part_d,     \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
                            st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
-                           np, meta, k, (unsigned long long *)qthr);                               \
+                           np, meta, k, (unsigned long long *)qthr, filt);                         \
     else                                                                                         \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP, 64>), grid, dim3(256), 0, s, part_d,     \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
                            st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
-                           np, meta, k, (unsigned long long *)qthr);                               \
+                           np, meta, k, (unsigned long long *)qthr, filt);                         \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
@@ -1839,7 +1945,7 @@ extern "C" int knn_launch_finalize(int dtype, int kp, const double *st_d, const 
                                    const int *st_i, const double *st_T, const void *qblk,
                                    size_t q_rows_pad, int nq, int n, int k, const double *meta,
                                    knn_neighbour_t *out, int *fail_count, int *fail_list,
-                                   int *mode_out, double *fbound, int force_fail, void *stream)
+                                   int *mode_out, double *fbound, int force_fail, int filt, void *stream)
 {
     if (k <= 0 || k > kp) return KNN_ERR_INVALID;
     const size_t off = q_rows_pad * knn_n_pad_dt(n, dtype);
@@ -1848,7 +1954,7 @@ extern "C" int knn_launch_finalize(int dtype, int kp, const double *st_d, const 
 #define CALL(T, KL, KP)                                                                        \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_finalize<T, KP>), grid, dim3(256), 0, s, st_d, st_x,   \
                        st_i, st_T, (const T *)qblk + off, nq, n, k, meta, out, fail_count,       \
-                       fail_list, mode_out, fbound, force_fail);                                 \
+                       fail_list, mode_out, fbound, force_fail, filt);                           \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL

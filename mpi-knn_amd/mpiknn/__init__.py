@@ -45,7 +45,7 @@ API_SYMBOLS = (
     "knn_ctx_contraction_bits", "knn_wire_bytes", "knn_wire_ok", "knn_wire_pack",
     "knn_wire_unpack", "knn_shadow_bytes", "knn_shadow_norm_offset", "knn_shadow_pack",
     "knn_ctx_shadow", "knn_ctx_step_shadow", "knn_ctx_begin_meta", "knn_ctx_shadow_bytes",
-    "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n",
+    "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n", "knn_ctx_split",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -107,6 +107,7 @@ def _load():
         "knn_search_packed": ([p, p, sz, p, p], i),
         "knn_ctx_info": ([p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], i),
         "knn_ctx_contraction_bits": ([p], i),
+        "knn_ctx_split": ([p], i),
         "knn_wire_bytes": ([sz, sz, i], sz),
         "knn_wire_ok": ([p], i),
         "knn_wire_pack": ([p, p, sz, sz, i, p], i),
@@ -376,5 +377,10 @@ class Context:
         return mode.value, splits.value
 
     def contraction_bits(self):
-        """64 / 32, 16 (exact fp16 MFMA) or 8 (exact int8 MFMA) for this search."""
+        """64 / 32, 16 (exact fp16 MFMA, or the split fp16 filter) or 8 (exact
+        int8 MFMA) for this search."""
         return lib.knn_ctx_contraction_bits(self._h)
+
+    def split(self):
+        """1 when this search filters with the split fp16 contraction."""
+        return lib.knn_ctx_split(self._h)

@@ -188,3 +188,63 @@ def test_f32_ring_blocks(knn, oracle, k):
                 e.step(engines[b].qb, blocks[b][1], blocks[b][0], rescan=True)
             e.rescan_end()
         assert_same(e.result(), full[base:base + rows], "f32 ring rank %d" % g)
+
+
+# ---- split fp16 filter (knn_ctx_split: fp32 GEMM mode) --------------------
+# The filter only chooses candidates; the exact fp64 re-rank and the
+# certificate (knn_cert_E with the split error bound) make the results those
+# of the oracle on the fp32-rounded points, bit for bit, and byte-identical
+# to the fp32 MFMA filter's (KNN_NO_SPLIT=1).
+
+def _split_case(X, k, monkeypatch, oracle):
+    import torch
+    import mpiknn.ring as ring
+    m, n = X.shape
+    e = ring.GpuEngine(torch, 0, n, m, m, k, dtype="f32")
+    e.pack(torch.from_numpy(np.ascontiguousarray(X.astype(np.float32))).to("cuda:0"), layout_col=False)
+    e.begin(0)
+    assert e.ctx.split() == 1, "expected the split fp16 filter"
+    got, _, u = run_engine(X.astype(np.float32), k)
+    assert_same(got, oracle.knn(rounded(X), k), "split f32 %dx%d k=%d" % (m, n, k))
+    monkeypatch.setenv("KNN_NO_SPLIT", "1")
+    base, _, ub = run_engine(X.astype(np.float32), k)
+    monkeypatch.delenv("KNN_NO_SPLIT")
+    assert got.tobytes() == base.tobytes()
+    return u, ub
+
+
+@pytest.mark.parametrize("m,n,k", [(2500, 960, 100), (3000, 128, 32), (1500, 40, 16), (2000, 333, 100)])
+def test_split_filter_gist_like(knn, oracle, monkeypatch, m, n, k):
+    X = datasets.gist_like(m, n, seed=m + n + k)
+    u, ub = _split_case(X, k, monkeypatch, oracle)
+    # the split filter's error bound is ~3.5x the fp32 filter's: a few more
+    # queries may miss the certificate (they take the exact rescan)
+    assert u <= 3 * ub + max(2, m // 50), "%d of %d queries uncertified (fp32 filter: %d)" % (u, m, ub)
+
+
+@pytest.mark.parametrize("scale", [1e-7, 3e-3, 1.0, 5e4, 2e9])
+def test_split_filter_scales(knn, oracle, monkeypatch, scale):
+    """The power-of-two pre-scale keeps hi in fp16 and lo normal for any
+    data magnitude; signed values, a few exact duplicates and near ties."""
+    rng = np.random.default_rng(5)
+    X = (rng.standard_normal((1200, 64)) * scale).astype(np.float32).astype(np.float64)
+    X[10] = X[3]
+    X[11] = X[3] * (1 + 2 ** -22)
+    _split_case(X, 30, monkeypatch, oracle)
+
+
+def test_split_filter_small_values_subnormal_lo(knn, oracle, monkeypatch):
+    """Values spanning 12 orders of magnitude: the lo halves of the small
+    ones are fp16 subnormals (the certificate's absolute term)."""
+    rng = np.random.default_rng(9)
+    X = rng.random((1500, 96)) * 10.0 ** rng.integers(-10, 2, (1500, 96))
+    _split_case(X, 24, monkeypatch, oracle)
+
+
+def test_split_filter_ring_loopback(knn, oracle, monkeypatch):
+    """P = 4 loopback ring (element blocks travel, each rank converts them to
+    split shadow rows) against the oracle."""
+    monkeypatch.setenv("KNN_RING_LOOPBACK", "1")
+    X = datasets.gist_like(2400, 200, seed=3)
+    got, _ = knn.search(X, 50, ngpus=4, dtype="f32")
+    assert_same(got, oracle.knn(rounded(X), 50), "split ring P=4")
