@@ -470,19 +470,25 @@ static int env_on(const char *name)
     return e && e[0] == '1';
 }
 
-/* The split fp16 filter serves fp32 searches in GEMM mode (knn_mode<float>:
- * finite, norms below 1e37, not the exact-integer INT mode, whose filter
- * must be exact).  Returns the pre-scale S = 2^(14 - e) with maxabs in
+/* The split fp16 filter serves searches in GEMM mode (knn_mode: finite,
+ * norms in range, not the exact-integer INT mode, whose filter must be
+ * exact), fp32 and fp64 blocks.  Returns the pre-scale S = 2^(14 - e) with maxabs in
  * [2^(e-1), 2^e), so maxabs S in [2^13, 2^14) fits fp16 with room, or 0
  * when the filter does not apply (S^2 must stay well inside fp32, and the
  * epilogue's -2 / S^2 too). */
 static float knn_split_scale(const double *meta, size_t n, int dtype)
 {
-    if (dtype != KNN_F32 || meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e37)) return 0.f;
     const double mx = meta[KNN_META_MAXABS];
-    const double rg = meta[KNN_META_MAXPOS] + meta[KNN_META_MAXNEG];
-    if (meta[KNN_META_NONINT] == 0.0 && (double)n * mx * mx <= 8388608.0 && (double)n * rg * rg <= 16777216.0)
-        return 0.f;   /* INT mode */
+    if (dtype == KNN_F32) {
+        const double rg = meta[KNN_META_MAXPOS] + meta[KNN_META_MAXNEG];
+        if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e37)) return 0.f;   /* SCAN */
+        if (meta[KNN_META_NONINT] == 0.0 && (double)n * mx * mx <= 8388608.0 && (double)n * rg * rg <= 16777216.0)
+            return 0.f;   /* INT mode */
+    } else {
+        if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e290)) return 0.f;   /* SCAN */
+        if (meta[KNN_META_NONINT] == 0.0 && mx * mx <= 2251799813685248.0 / (4.0 * (double)n))
+            return 0.f;   /* INT mode */
+    }
     if (!(mx > 0.0)) return 0.f;
     int e = 0;
     (void)frexp(mx, &e);
@@ -559,7 +565,7 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
             if (hipMalloc(&c->qsp, need) != hipSuccess) return KNN_ERR_NOMEM;
             c->qsp_bytes = need;
         }
-        RCHK(knn_launch_shadow_split(c->qsp, d_qblock, c->q_rows_pad, c->n, c->sscale, stream));
+        RCHK(knn_launch_shadow_split(c->qsp, d_qblock, c->dtype, c->q_rows_pad, c->n, c->sscale, stream));
     } else if (c->shadow) {
         const size_t need = c->q_rows_pad * knn_round_up(c->n, 64) * 2;
         if (need > c->qsh_bytes) {
@@ -907,7 +913,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
                 c->csp_bytes = need;
             }
             if (!c->csp[set] && hipMalloc(&c->csp[set], c->csp_bytes) != hipSuccess) return KNN_ERR_NOMEM;
-            RCHK(knn_launch_shadow_split(c->csp[set], d_cblock, knn_rows_pad(nc), c->n, c->sscale, ds));
+            RCHK(knn_launch_shadow_split(c->csp[set], d_cblock, c->dtype, knn_rows_pad(nc), c->n, c->sscale, ds));
             csh = c->csp[set];
         }
     } else if (d_sblock) {

@@ -122,11 +122,12 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
 /* fp16 shadow rows (round_up(n, 64) halves a row) of a packed block */
 int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
-/* split fp16 shadow rows of an fp32 block: per 32 features 32 halves hi =
+/* split fp16 shadow rows of an fp32 / fp64 block: per 32 features 32 halves hi =
  * RN16(S x), then 32 halves lo = RN16(S x - hi); rows of round_up(n, 32) * 4
  * bytes; S a power of two (knn_engine.c: maxabs S in [2^13, 2^14)) */
 static inline size_t knn_split_rs(size_t n) { return knn_round_up(n ? n : 1, 32) * 4; }
-int knn_launch_shadow_split(void *dst, const void *blk, size_t rows_pad, size_t n, float S, void *stream);
+int knn_launch_shadow_split(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, float S,
+                            void *stream);
 /* knn_i8.hip: element block -> byte block (meta = the reduced meta) and the
  * int8 distance + top-k kernel (partial lists [split][query][2][kl]) */
 int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,

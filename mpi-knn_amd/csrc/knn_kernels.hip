@@ -164,12 +164,14 @@ __device__ __forceinline__ double knn_exact_sq_v(const T *__restrict__ a, const 
 //   hi.hi + hi.lo + lo.hi on v_mfma_f32_16x16x32_f16.  Per element
 //   |xS - hi - lo| <= 2^-22 |xS| + 2^-25 and the dropped lo.lo <=
 //   2^-22 |q_j c_j| (+ subnormal terms): 3 2^-22 sum|q_j c_j|, 12u qc for d^2.
-//   fp16 products are exact in fp32; the accumulator sums n hi.hi products
-//   and n/32 per-chunk cross-term sums (any order, fp32: <= 1.05 n u
-//   sum|terms|), 1.05 n u qc for d^2; norms, qn + cn and the final fma 4u
-//   qc.  With a 20% margin on the accumulation (the MFMA's internal order
-//   is not specified; its precision is at least fp32): ((1.25 n + 24) u +
-//   4 (n+4) 2^-53) qc.  Subnormal fp16 halves may be flushed by the MFMA:
+//   fp16 products are exact in fp32; each 32-feature chunk's 96 products
+//   are summed apart in fp32 (any order: <= 95u sum|chunk terms|) and the
+//   n/32 chunk sums added to the accumulator (fp32: <= (n/32) u sum|q_j
+//   c_j|; fp64 blocks: fp64, negligible), so d^2 is off by (97 + n/32) 1.01
+//   u qc; norms, qn + cn and the final fma 4u qc.  With a 20% margin (the
+//   MFMA's internal order is not specified; its precision is at least
+//   fp32): ((136 + n/25) u + 4 (n+4) 2^-53) qc (fp64 blocks without the n
+//   term).  Subnormal fp16 halves may be flushed by the MFMA:
 //   then up to 2^-14 / S <= 2^-27 maxabs is lost per element, the absolute
 //   part 2^-26 maxabs sqrt(n) (|q| + |c|).  The fp32 filter's is ~ (n + 4)
 //   u qc.
@@ -181,7 +183,9 @@ __device__ __forceinline__ double knn_cert_E(int n, double qn, double maxnorm, i
     const double nn = (double)n + 4.0, qc = qn + maxnorm;
     if (split) {
         const double ul = 5.9604644775390625e-08;   // 2^-24
-        return ((1.25 * n + 24.0) * ul + 4.0 * nn * 1.1102230246251565e-16) * qc * (1.0 + 1e-6) +
+        // fp32 blocks add the n/32 chunk sums in fp32, fp64 blocks in fp64
+        const double acc = sizeof(TE) == 4 ? (double)n / 25.0 : (double)n * 1e-8;
+        return ((136.0 + acc) * ul + 4.0 * nn * 1.1102230246251565e-16) * qc * (1.0 + 1e-6) +
                1.4901161193847656e-08 * maxabs * sqrt((double)n) * (sqrt(qn) + sqrt(maxnorm));
     }
     if constexpr (sizeof(TE) == 8) return 8.0 * nn * u * qc;
@@ -376,14 +380,15 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     // H16 2: qblk / cblk are fp16 shadow rows (k_shadow), n_pad their row
     // length; the norms stay in the element blocks
     // H16 3: split fp16 shadow rows (knn_shadow_split, 4 bytes a feature:
-    // per 32 features 32 hi halves then 32 lo halves), fp32 blocks only
-    static_assert(H16 != 3 || sizeof(T) == 4, "split fp16 filter: fp32 blocks");
+    // per 32 features 32 hi halves then 32 lo halves); fp64 blocks keep
+    // their fp64 accumulators (in the fp32 MFMA layout)
     constexpr int RS = H16 == 2 ? 2 : (H16 == 3 ? 4 : (int)sizeof(T));   // bytes per staged element
     constexpr int BK = 128 / RS;                      // features per 128-B chunk
     // fp64 H16 (knn_to_h4): the fp32 MFMA output layout, row 4g + r of a
     // 16-row m-tile in lane group g, register r, instead of fp64's g + 4r
     constexpr bool H16D = H16 != 0 && H16 != 3 && sizeof(T) == 8;
-    auto rowmap = [](int gg, int r) { return H16D ? 4 * gg + r : KT<T>::row(gg, r); };
+    constexpr bool F32L = H16 != 0 && sizeof(T) == 8;   // fp64 accumulators, fp32 MFMA layout
+    auto rowmap = [](int gg, int r) { return F32L ? 4 * gg + r : KT<T>::row(gg, r); };
     constexpr int ES = (int)sizeof(T);
     typedef typename KT<T>::acc_t acc_t;
     typedef typename KT<T>::frag_t frag_t;
@@ -758,14 +763,15 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                     for (int mt = 0; mt < 8; mt++) {
                         const knn_h8 ah = *(const LDS_AS knn_h8 *)(cs + mt * 2048 + fslot);
                         const knn_h8 al = *(const LDS_AS knn_h8 *)(cs + mt * 2048 + fslot1);
-                        // the cross terms (~2^-11 of hi.hi) summed apart and
-                        // added once a chunk: the accumulator's rounding then
-                        // runs over n hi.hi products + n/32 small terms, not
-                        // 3n (knn_cert_E, split)
+                        // a chunk's 96 products summed apart (cross terms
+                        // first), then added to the accumulator: its rounding
+                        // runs over n/32 chunk sums, not 3n products
+                        // (knn_cert_E, split); fp64 blocks add them in fp64
                         flt4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ql, (flt4){0, 0, 0, 0}, 0, 0, 0);
                         t = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, qh, t, 0, 0, 0);
-                        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qh, acc[mt], 0, 0, 0);
-                        acc[mt] += t;
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qh, t, 0, 0, 0);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) acc[mt][r] += (T)t[r];
                     }
                     advance();
                     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -1725,21 +1731,24 @@ extern "C" int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t r
 // 32-feature group, the 32 halves hi = RN16(S x) then the 32 halves lo =
 // RN16(S x - hi) (S x - hi is exact in fp32: Sterbenz); zero past n.  One
 // thread per 8 features: a 16-byte hi and a 16-byte lo store.
-__global__ __launch_bounds__(256) void k_shadow_split(char *__restrict__ dst, const float *__restrict__ src,
+template <typename T>
+__global__ __launch_bounds__(256) void k_shadow_split(char *__restrict__ dst, const T *__restrict__ src,
                                                       size_t rows, int n, int nps, int npd, float S)
 {
     const size_t per = (size_t)npd / 8, tot = rows * per;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < tot; i += (size_t)gridDim.x * 256) {
         const size_t r = i / per;
         const int j0 = (int)(i - r * per) * 8;
-        const float *row = src + r * (size_t)nps;
+        const T *row = src + r * (size_t)nps;
         knn_h8 hi, lo;
 #pragma unroll
         for (int e = 0; e < 8; e++) {
-            const float x = j0 + e < n ? row[j0 + e] * S : 0.f;
-            const _Float16 h = (_Float16)x;
+            // fp64: x S - hi exact in fp64, rounded once to fp16 (through
+            // fp32: exact, |x S - hi| has <= 24 significant bits below hi's)
+            const T x = j0 + e < n ? row[j0 + e] * (T)S : (T)0;
+            const _Float16 h = (_Float16)(float)x;
             hi[e] = h;
-            lo[e] = (_Float16)(x - (float)h);
+            lo[e] = (_Float16)(float)(x - (T)(float)h);
         }
         char *o = dst + r * (size_t)npd * 4 + (size_t)(j0 >> 5) * 128 + 2 * (j0 & 31);
         *(knn_h8 *)o = hi;
@@ -1747,14 +1756,20 @@ __global__ __launch_bounds__(256) void k_shadow_split(char *__restrict__ dst, co
     }
 }
 
-extern "C" int knn_launch_shadow_split(void *dst, const void *blk, size_t rows_pad, size_t n, float S,
-                                       void *stream)
+extern "C" int knn_launch_shadow_split(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,
+                                       float S, void *stream)
 {
-    const int npd = (int)knn_round_up(n, 32), nps = (int)knn_n_pad_dt(n, KNN_F32);
+    const int npd = (int)knn_round_up(n, 32), nps = (int)knn_n_pad_dt(n, dtype);
     const size_t tot = rows_pad * (size_t)npd / 8;
     const unsigned grid = (unsigned)(tot / 256 + 1 < 8192 ? tot / 256 + 1 : 8192);
-    hipLaunchKernelGGL(k_shadow_split, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char *)dst,
-                       (const float *)blk, rows_pad, (int)n, nps, npd, S);
+    if (dtype == KNN_F32)
+        hipLaunchKernelGGL(k_shadow_split<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char *)dst,
+                           (const float *)blk, rows_pad, (int)n, nps, npd, S);
+    else if (dtype == KNN_F64)
+        hipLaunchKernelGGL(k_shadow_split<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char *)dst,
+                           (const double *)blk, rows_pad, (int)n, nps, npd, S);
+    else
+        return KNN_ERR_INVALID;
     return hip_status();
 }
 
@@ -1815,6 +1830,10 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     int uj_int = (k + 1 + 3) / 4 - 1;
     if (uj_int > KL - 1) uj_int = KL - 1;
     int uj_gemm = KP / 4 - 1 > uj_int ? KP / 4 - 1 : uj_int;
+    // split fp16 filter: its error margin is ~2^-24 relative, not 2^-53, so
+    // the published bound sits at the lanes' last entries (more distance
+    // between the k-th and the bound for the certificate)
+    if (flags & KNN_DIST_SPLIT) uj_gemm = KL - 1;
     if (uj_gemm > KL - 1) uj_gemm = KL - 1;
     const int uj = uj_int | (uj_gemm << 8);
     // geometry checks the kernel relies on (no out-of-bounds staging)
@@ -1828,16 +1847,13 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     if (flags & KNN_DIST_SPLIT) {
         // split fp16 shadow rows (4 bytes a feature); m2s = -2 / S^2 undoes
         // the scaling in the epilogue's fma (a power of two: exact)
-        if constexpr (sizeof(T) == 4) {
-            if (!qsh || !csh) return KNN_ERR_INVALID;
-            const int nps = (int)knn_round_up((size_t)n, 32);
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 3>), grid, dim3(512), 0, s,
-                               (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
-                               nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                               (unsigned long long *)qthr, uj, xord, m2s);
-            return hip_status();
-        }
-        return KNN_ERR_INVALID;
+        if (!qsh || !csh) return KNN_ERR_INVALID;
+        const int nps = (int)knn_round_up((size_t)n, 32);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 3>), grid, dim3(512), 0, s,
+                           (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
+                           nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
+                           (unsigned long long *)qthr, uj, xord, m2s);
+        return hip_status();
     }
     if ((flags & KNN_DIST_SHADOW) && (flags & KNN_DIST_H16)) {
         if (!qsh || !csh) return KNN_ERR_INVALID;

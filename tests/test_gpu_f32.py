@@ -248,3 +248,23 @@ def test_split_filter_ring_loopback(knn, oracle, monkeypatch):
     X = datasets.gist_like(2400, 200, seed=3)
     got, _ = knn.search(X, 50, ngpus=4, dtype="f32")
     assert_same(got, oracle.knn(rounded(X), 50), "split ring P=4")
+
+
+@pytest.mark.parametrize("m,n", [(3000, 784), (2000, 100)])
+def test_split_filter_fp64_blocks(knn, oracle, monkeypatch, m, n):
+    """fp64 GEMM mode (SURVEY C1's real-valued data) on the split filter:
+    bit-exact vs the oracle (the reference's fp64 S) and byte-identical to
+    the fp64 MFMA filter (KNN_NO_SPLIT=1)."""
+    X, _ = datasets.mnist_real(m, n)
+    import torch
+    import mpiknn.ring as ring
+    e = ring.GpuEngine(torch, 0, n, m, m, 30, dtype="f64")
+    e.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
+    e.begin(0)
+    assert e.ctx.split() == 1
+    got, _, u = run_engine(X, 30, dtype="f64")
+    assert_same(got, oracle.knn(X, 30), "split f64 %dx%d" % (m, n))
+    monkeypatch.setenv("KNN_NO_SPLIT", "1")
+    base, _, ub = run_engine(X, 30, dtype="f64")
+    assert got.tobytes() == base.tobytes()
+    assert u <= ub + max(2, m // 200)
