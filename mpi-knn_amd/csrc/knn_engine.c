@@ -75,6 +75,8 @@ struct knn_ctx {
     int nstep;
     /* per-query filter bound shared by all splits and ring steps */
     double *qthr;
+    /* int8 kernel: per query 4 cross-split summary slots (k_dist_topk_i8) */
+    unsigned long long *qsum;
     /* running state per query: KNN_KP x (approx d^2, exact S, idx), T pair */
     double *st_d, *st_x, *st_T;
     int *st_i;
@@ -254,6 +256,7 @@ static void ctx_free_buffers(knn_ctx_t *c)
     for (int b = 0; b < KNN_PSETS; b++) hipFree(c->csp[b]);
     if (c->ev_in) hipEventDestroy(c->ev_in);
     hipFree(c->qthr);
+    hipFree(c->qsum);
     hipFree(c->st_d);
     hipFree(c->st_x);
     hipFree(c->st_T);
@@ -367,6 +370,7 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     const size_t np = c->nq_pad;
     int ok = 1;
     ok &= hipMalloc((void **)&c->qthr, np * sizeof(double)) == hipSuccess;
+    ok &= hipMalloc((void **)&c->qsum, np * 4 * sizeof(unsigned long long)) == hipSuccess;
     ok &= hipMalloc((void **)&c->st_d, np * c->kp * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->st_x, np * c->kp * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->st_i, np * c->kp * sizeof(int)) == hipSuccess;
@@ -580,6 +584,8 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
     }
     HIPCHK(hipMemsetAsync(c->fail_count, 0, sizeof(int), (hipStream_t)stream));
     RCHK(knn_launch_fill_inf(c->qthr, (int)c->nq_pad, stream));
+    if (c->i8)   /* 0x7f7f7f7f: above every int8-mode d^2 (an empty summary) */
+        HIPCHK(hipMemsetAsync(c->qsum, 0x7f, c->nq_pad * 4 * sizeof(unsigned long long), (hipStream_t)stream));
     return KNN_OK;
 }
 
@@ -944,7 +950,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
         }
         RCHK(knn_launch_dist_i8(c->kp, c->klx, c->k, c->qs8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
                                 knn_rows_pad(c->block_cap), (int)c->n, nsplit, c->part_d[set],
-                                c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr, ds));
+                                c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr, c->qsum, ds));
     } else
         RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq,
                                   cblk, knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta,

@@ -293,15 +293,15 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     const knn_i8_blocks_t cb, size_t c_rows_pad, int rs,
     int nks, int ntiles, int nsplit, int nqb, double *__restrict__ part_d,
     int *__restrict__ part_i, double *__restrict__ part_T, int nq_pad,
-    unsigned long long *__restrict__ qthr, int uj)
+    unsigned long long *__restrict__ qthr, int uj, unsigned long long *__restrict__ qsum)
 {
     constexpr int MB = 16 / W;              // m-blocks per wave
     constexpr int PW = 16 / W;              // DMA pieces per wave per chunk
     constexpr int LPQ = 2 * (W / 4);        // lists per query
     constexpr int NORM0 = NST * 16384;
     constexpr int BUF0 = NORM0 + NST * 512; // [W][NB][64] survivor d^2, then ids
-    constexpr int XB0 = BUF0 + 2 * W * NB * 256;   // W = 8: [8][32] bound exchange
-    constexpr int TB0 = XB0 + (W == 8 ? 8 * 32 * 4 : 0);   // block table
+    constexpr int XB0 = BUF0 + 2 * W * NB * 256;   // W = 8: [8][32] bound exchange (u4, v8, v16)
+    constexpr int TB0 = XB0 + (W == 8 ? 3 * 8 * 32 * 4 : 0);   // block table
     constexpr int LDSB = TB0 + (int)((sizeof(i8_tab_lds) + 15) / 16 * 16);
     __shared__ __attribute__((aligned(16))) char smem[LDSB];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // (W = 8: the query's lanes in both waves; second byte)
     const int ujm = (uj & 255) < KL - 1 ? (uj & 255) : KL - 1;
     const int uj4 = ((uj >> 8) & 255) < KL - 1 ? ((uj >> 8) & 255) : KL - 1;
-    LDS_AS int *xb = (LDS_AS int *)(smem + XB0);
+    LDS_AS int *xb = (LDS_AS int *)(smem + XB0);   // [3][8 waves][32]: u4, v8, v16
     LDS_AS int *bk = (LDS_AS int *)(smem + BUF0) + wave_s * NB * 64 + lane;   // entry e at bk[64 e]
     LDS_AS int *bi = bk + W * NB * 64;
     int cnt = 0;   // buffered survivors of this lane
@@ -379,7 +379,10 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         tab->nblk = cb.nblk;
     }
     if constexpr (W == 8) {
-        if (h == 0) xb[wave_s * 32 + r32] = I8_INF;
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) xb[256 * j + wave_s * 32 + r32] = I8_INF;
+        }
     }
     __syncthreads();
 
@@ -450,6 +453,27 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // 4(uj4+1) >= k+1 entries <= the max of their L[uj4]; the partner wave's
     // half comes through LDS, lock-free -- a stale value is larger (lists
     // only shrink), so the max stays a valid bound, only a looser one.
+    // Cross-split summaries (W = 8, k + 1 <= 32): splits of one launch cover
+    // disjoint rows, so 4 splits' v8 (8 rows each) or 2 splits' v16 bound
+    // the query's (k+1)-th d^2 -- over the union of their rows, 4x the rows
+    // behind one split's own 4-lane bound.  Split s keeps (v8 << 32 | v16)
+    // in slot s & 3 of qsum[query][4] (atomic min of the packed pair: a slot
+    // holds one split's consistent pair, the smaller v8); every split reads
+    // the 4 slots with the qthr re-read.  Publication is rate-limited: the
+    // atomic stays counted in vmcnt (~2-3k cycles) and the ring's next
+    // counted wait would sit it out.
+    // (the 12-entry-list kernels only: the 17-entry ones have no registers
+    // to spare at 28 K-steps)
+    constexpr bool SUM = W == 8 && KL == KNN_I8_KL_S;
+    int q_pubx = -1000;
+    auto qsum_publish = [&](int v8, int v16) {
+        if (!SUM || qsum == nullptr || rh != 0 || h != 0 || myq >= nq) return;
+        if (v8 >= I8_INF || s_x - q_pubx < 4 * nch) return;
+        q_pubx = s_x;
+        const unsigned long long val = ((unsigned long long)(unsigned)v8 << 32) | (unsigned)v16;
+        unsigned long long *pq = qsum + (size_t)myq * 4 + (split & 3);
+        asm volatile("global_atomic_umin_x2 %0, %1, off" ::"v"(pq), "v"(val) : "memory");
+    };
     auto refresh = [&]() {
         int lmin = L[KL - 1], u = L[0], u4 = L[0];
 #pragma unroll
@@ -467,10 +491,27 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         int nb = lmin < u ? lmin : u;
         if (uj & (1 << 16)) nb = lmin;
         if constexpr (W == 8) {
+            // the split's summary for the other splits: v8 / v16 = the max
+            // over the query's 4 lanes of L[1] / L[3] -- 8 / 16 rows of this
+            // split lie at or below them
             if (h == 0) xb[wave_s * 32 + r32] = u4;
             const int pu = xb[(wave_s ^ 4) * 32 + r32];
             u4 = pu > u4 ? pu : u4;
             nb = u4 < nb ? u4 : nb;
+            if constexpr (SUM) {
+                int v8 = L[1], v16 = L[3];
+                const int v8o = __shfl_xor(v8, 32), v16o = __shfl_xor(v16, 32);
+                v8 = v8o > v8 ? v8o : v8;
+                v16 = v16o > v16 ? v16o : v16;
+                if (h == 0) {
+                    xb[256 + wave_s * 32 + r32] = v8;
+                    xb[512 + wave_s * 32 + r32] = v16;
+                }
+                const int p8 = xb[256 + (wave_s ^ 4) * 32 + r32], p16 = xb[512 + (wave_s ^ 4) * 32 + r32];
+                v8 = p8 > v8 ? p8 : v8;
+                v16 = p16 > v16 ? p16 : v16;
+                qsum_publish(v8, v16);
+            }
         }
         thr = nb < thr ? nb : thr;
     };
@@ -503,16 +544,34 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // at an epilogue with xdone > X0 the wait before barrier B(xdone) (or,
     // on the last tile, B(total - 1) >= X0) has seen stage X0 land.
     unsigned long long q_bits = 0x7ff0000000000000ull;
+    knn_v4i qs0 = {I8_INF, I8_INF, I8_INF, I8_INF}, qs1 = qs0;   // qsum slots 0-1, 2-3
     int q_ready = -1;   // -1: no load pending
     auto qthr_issue = [&](int xnow) {
         const unsigned long long *pq = qthr + myq;
         asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(q_bits) : "v"(pq) : "memory");
+        if (SUM && qsum != nullptr) {
+            const unsigned long long *ps = qsum + (size_t)myq * 4;
+            asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(qs0) : "v"(ps) : "memory");
+            asm volatile("global_load_dwordx4 %0, %1, off offset:16 sc1" : "=v"(qs1) : "v"(ps) : "memory");
+        }
         q_ready = xnow;
     };
     auto qthr_apply = [&]() {
         asm volatile("" : "+v"(q_bits));
+        if constexpr (SUM) asm volatile("" : "+v"(qs0), "+v"(qs1));
         const double td = __longlong_as_double((long long)q_bits);
-        const int tq = td >= 2147483647.0 ? I8_INF : (int)td;
+        int tq = td >= 2147483647.0 ? I8_INF : (int)td;
+        if (SUM && qsum != nullptr) {
+            // slot s = (v16, v8) as (lo, hi) dwords: qs0 = {v16_0, v8_0, v16_1, v8_1}
+            const int a8 = qs0.y > qs0.w ? qs0.y : qs0.w, b8 = qs1.y > qs1.w ? qs1.y : qs1.w;
+            const int b4 = a8 > b8 ? a8 : b8;                        // 4 splits x 8 rows
+            const int s1 = qs0.x < qs0.z ? qs0.x : qs0.z, l1 = qs0.x < qs0.z ? qs0.z : qs0.x;
+            const int s2 = qs1.x < qs1.z ? qs1.x : qs1.z, l2 = qs1.x < qs1.z ? qs1.z : qs1.x;
+            const int m1 = s1 > s2 ? s1 : s2, m2 = l1 < l2 ? l1 : l2;
+            const int b2 = m1 < m2 ? m1 : m2;                        // 2nd smallest v16: 2 x 16 rows
+            const int bs = b4 < b2 ? b4 : b2;
+            tq = bs < tq ? bs : tq;
+        }
         thr = tq < thr ? tq : thr;
         q_ready = -1;
     };
@@ -714,17 +773,18 @@ template <int KL, int NKS, int W, int WPS, int NST, int NB>
 static void launch_i8(dim3 grid, hipStream_t s, const void *qsh, size_t q_rows_pad, size_t q_base,
                       int nq, const knn_i8_blocks_t &cb, size_t c_rows_pad, int rs,
                       int nks, int ntiles, int nsplit, int nqb, double *part_d, int *part_i,
-                      double *part_T, int nq_pad, double *qthr, int uj)
+                      double *part_T, int nq_pad, double *qthr, int uj, unsigned long long *qsum)
 {
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KL, NKS, W, WPS, NST, NB>), grid, dim3(64 * W), 0, s,
                        (const signed char *)qsh, q_rows_pad, q_base, nq, cb, c_rows_pad, rs, nks, ntiles,
-                       nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj);
+                       nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj,
+                       W == 8 ? qsum : nullptr);
 }
 
 extern "C" int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t q_rows_pad, size_t q_base,
                                   int nq, const knn_i8_blocks_t *cbp, size_t c_rows_pad, int n,
                                   int nsplit, double *part_d, int *part_i, double *part_T,
-                                  int nq_pad, double *qthr, void *stream)
+                                  int nq_pad, double *qthr, unsigned long long *qsum, void *stream)
 {
     const int rs = (int)knn_s8_rs((size_t)n), nks = rs / 32;
     const int nqb = (nq + 127) / 128;
@@ -759,8 +819,10 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t
     if (no2) uj |= 1 << 16;
     const dim3 grid((unsigned)(nqb * nsplit));
     hipStream_t s = (hipStream_t)stream;
+    // cross-split summaries combine 4 x 8 or 2 x 16 rows: for k + 1 <= 32
+    if (k + 1 > 32) qsum = nullptr;
 #define I8_ARGS grid, s, qsh, q_rows_pad, q_base, nq, cb, c_rows_pad, rs, nks, ntiles, nsplit, \
-                nqb, part_d, part_i, part_T, nq_pad, qthr, uj
+                nqb, part_d, part_i, part_T, nq_pad, qthr, uj, qsum
     // One workgroup a CU (queries in up to 112 VGPRs), an 8-stage ring.
     // k <= 32: 8 waves (two a SIMD, 2 m-blocks each, 4 lists a query) and
     // 6-entry survivor buffers (merging sooner tightens the bounds sooner:

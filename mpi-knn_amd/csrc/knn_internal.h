@@ -135,7 +135,7 @@ int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t rows_pad, s
 int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t q_rows_pad, size_t q_base, int nq,
                        const knn_i8_blocks_t *cb, size_t c_rows_pad, int n, int nsplit,
                        double *part_d, int *part_i, double *part_T, int nq_pad, double *qthr,
-                       void *stream);
+                       unsigned long long *qsum, void *stream);
 int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *part_i,
                      const double *part_T, int nsplit, int lpq, int kl, int nq, int nq_pad,
                      int first_step,

@@ -38,7 +38,8 @@ static void kb8_go(dim3 grid, const void *qsh, size_t q_rows_pad, int nq, const 
     cb.t0[0] = 0;
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KNN_I8_KL_S, NKS, 8, 2, NST, NB>), grid, dim3(512), 0, 0,
                        (const signed char *)qsh, q_rows_pad, (size_t)0, nq, cb, c_rows_pad, rs, nks, ntiles,
-                       nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj);
+                       nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj,
+                       (unsigned long long *)nullptr);
 }
 
 // average kernel ms over iters launches (after one warm-up); reset: 1 bounds
