@@ -610,7 +610,13 @@ int knn_ctx_shadow_pack(knn_ctx_t *c, void *d_sblock, const void *d_block, size_
     if (c->shadow != 2) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     const size_t rp = knn_rows_pad(cap);
-    RCHK(knn_launch_shadow8(d_sblock, d_block, c->dtype, rp, c->n, c->meta, stream));
+    if (d_block == c->qblk && rp == c->q_rows_pad && c->qs8) {
+        /* the query block (a ring's own block): begin converted it already */
+        HIPCHK(hipMemcpyAsync(d_sblock, c->qs8, knn_s8_norm_offset(cap, c->n) + rp * 4, hipMemcpyDeviceToDevice,
+                              (hipStream_t)stream));
+    } else {
+        RCHK(knn_launch_shadow8(d_sblock, d_block, c->dtype, rp, c->n, c->meta, stream));
+    }
     HIPCHK(hipMemcpyAsync((char *)d_sblock + knn_s8_norm_offset(cap, c->n) + rp * 4,
                           (const char *)d_block + knn_block_meta_offset_dt(cap, c->n, c->dtype),
                           KNN_META_DOUBLES * sizeof(double), hipMemcpyDeviceToDevice,

@@ -70,8 +70,11 @@ def test_h16_not_taken_above_2048(oracle):
     check(oracle, X, 8, 32)
 
 
-def test_h16_not_taken_real_valued(oracle):
+def test_h16_not_taken_real_valued(oracle, monkeypatch):
+    """Real-valued data never takes the exact fp16 contraction: it runs the
+    split fp16 filter (knn_ctx_split) or, without it, fp32 MFMA."""
     X = datasets.digits_real()[0]
+    monkeypatch.setenv("KNN_NO_SPLIT", "1")
     check(oracle, X, 30, 32)
 
 
@@ -90,11 +93,12 @@ def test_h16_fp64_signed_boundary(oracle):
     check(oracle, X, 32, 16, "f64")
 
 
-def test_h16_fp64_not_taken(oracle):
+def test_h16_fp64_not_taken(oracle, monkeypatch):
     rng = np.random.default_rng(9)
     X = rng.integers(0, 258, (2000, 50)).astype(np.float64)
     X[0, 0] = 257.0
     check(oracle, X, 30, 64, "f64")
+    monkeypatch.setenv("KNN_NO_SPLIT", "1")   # (real-valued: the split fp16 filter otherwise)
     check(oracle, datasets.digits_real()[0], 30, 64, "f64")
 
 
