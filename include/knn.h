@@ -293,7 +293,10 @@ KNN_API int knn_ctx_step_shadow_n(knn_ctx_t *ctx, int nblk, const void *const *d
 /* Finish: write nq*k records to d_out.  Returns in *unresolved (host; the
  * call synchronises the stream) the number of queries whose candidate set
  * could not be certified exact; if > 0 the caller runs one more pass over
- * every block with knn_ctx_rescan_step() then knn_ctx_rescan_end(). */
+ * every block with knn_ctx_rescan_step() then knn_ctx_rescan_end().  The
+ * records are written behind the last merge on the context's own stream,
+ * not after work pending on `stream`: d_out must not be in use by pending
+ * work; `stream` is ordered after the records on return. */
 KNN_API int knn_ctx_end(knn_ctx_t *ctx, knn_neighbour_t *d_out, size_t *unresolved,
                 void *stream);
 KNN_API int knn_ctx_rescan_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,

@@ -71,7 +71,7 @@ struct knn_ctx {
     /* overlapped step schedule (knn_ctx_step): distance kernels alternate
      * over two streams, merges run in order on a third */
     hipStream_t ds[2], ms;
-    hipEvent_t ev_in, ev_d[2], ev_m[KNN_PSETS], ev_ds[KNN_PSETS];
+    hipEvent_t ev_in, ev_d[2], ev_m[KNN_PSETS], ev_ds[KNN_PSETS], ev_end;
     int nstep;
     /* per-query filter bound shared by all splits and ring steps */
     double *qthr;
@@ -255,6 +255,7 @@ static void ctx_free_buffers(knn_ctx_t *c)
     hipFree(c->qsp);
     for (int b = 0; b < KNN_PSETS; b++) hipFree(c->csp[b]);
     if (c->ev_in) hipEventDestroy(c->ev_in);
+    if (c->ev_end) hipEventDestroy(c->ev_end);
     hipFree(c->qthr);
     hipFree(c->qsum);
     hipFree(c->st_d);
@@ -264,7 +265,6 @@ static void ctx_free_buffers(knn_ctx_t *c)
     hipFree(c->fail_count);
     hipFree(c->fail_list);
     hipFree(c->fbound);
-    hipFree(c->mode_dev);
     hipFree(c->rs_d);
     hipFree(c->rs_i);
     for (int i = 0; i < 3 * KNN_PROF_STEPS; i++)
@@ -375,10 +375,11 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     ok &= hipMalloc((void **)&c->st_x, np * c->kp * sizeof(double)) == hipSuccess;
     ok &= hipMalloc((void **)&c->st_i, np * c->kp * sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->st_T, np * 2 * sizeof(double)) == hipSuccess;
-    ok &= hipMalloc((void **)&c->fail_count, sizeof(int)) == hipSuccess;
+    /* [0] unresolved queries, [1] mode: one allocation, one read-back */
+    ok &= hipMalloc((void **)&c->fail_count, 2 * sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->fail_list, np * sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->fbound, np * sizeof(double)) == hipSuccess;
-    ok &= hipMalloc((void **)&c->mode_dev, sizeof(int)) == hipSuccess;
+    if (ok) c->mode_dev = c->fail_count + 1;
     for (int b = 0; b < 2; b++) {
         ok &= hipStreamCreateWithFlags(&c->ds[b], hipStreamNonBlocking) == hipSuccess;
         ok &= hipEventCreateWithFlags(&c->ev_d[b], hipEventDisableTiming) == hipSuccess;
@@ -392,6 +393,7 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     ok &= hipStreamCreateWithPriority(&c->ms, hipStreamNonBlocking, prio_hi) == hipSuccess;
     ok &= hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) == hipSuccess;
+    ok &= hipEventCreateWithFlags(&c->ev_end, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         ctx_free_buffers(c);
         free(c);
@@ -582,10 +584,10 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
         }
         RCHK(knn_launch_shadow(c->qsh, d_qblock, c->dtype, c->q_rows_pad, c->n, stream));
     }
-    HIPCHK(hipMemsetAsync(c->fail_count, 0, sizeof(int), (hipStream_t)stream));
-    RCHK(knn_launch_fill_inf(c->qthr, (int)c->nq_pad, stream));
-    if (c->i8)   /* 0x7f7f7f7f: above every int8-mode d^2 (an empty summary) */
-        HIPCHK(hipMemsetAsync(c->qsum, 0x7f, c->nq_pad * 4 * sizeof(unsigned long long), (hipStream_t)stream));
+    /* fail_count and mode_dev are one allocation: one launch resets both,
+     * the bounds and (int8: 0x7f7f7f7f, above every int8-mode d^2 -- an
+     * empty summary) the cross-split summaries */
+    RCHK(knn_launch_begin_init(c->qthr, c->i8 ? c->qsum : NULL, (int)c->nq_pad, c->fail_count, stream));
     return KNN_OK;
 }
 
@@ -786,10 +788,17 @@ static int ensure_part_buffers(knn_ctx_t *c, int nsplit, int set, int off)
 static int launch_merge_sets(knn_ctx_t *c, int set, int nsets, int nsplit_total, const void *cblk,
                              size_t c_base, size_t nc)
 {
-    RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
-                          nsplit_total, c->lpq, c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x,
-                          c->st_i, c->st_T, c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n,
-                          c->meta, c->qthr, c->split, c->ms));
+    /* int8 lists (exact INT-mode keys, k <= 32): the rank merge */
+    if (c->i8 && c->kp <= KNN_KP_M && (c->klx == KNN_I8_KL_S || c->klx == KNN_I8_KL) &&
+        c->lpq * nsplit_total <= 64 && !env_on("KNN_NO_RANK_MERGE"))
+        RCHK(knn_launch_merge_rank(c->dtype, c->kp, c->klx, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
+                                   nsplit_total, c->lpq, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d,
+                                   c->st_x, c->st_i, c->st_T, c->qthr, c->ms));
+    else
+        RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
+                              nsplit_total, c->lpq, c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x,
+                              c->st_i, c->st_T, c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n,
+                              c->meta, c->qthr, c->split, c->ms));
     c->merged = 1;
     for (int x = 0; x < nsets; x++) HIPCHK(hipEventRecord(c->ev_m[(set + x) % KNN_PSETS], c->ms));
     return KNN_OK;
@@ -811,7 +820,7 @@ static int merge_pending(knn_ctx_t *c)
  *   ds[s%2]: wait ev_in (the caller's stream at this call: the block has
  *            arrived, begin() is done) and ev_m[p] (merge s-4 has read the
  *            partial set), then k_dist_topk(s)              -> ev_d[s%2]
- *   ms:      wait ev_d[s%2] and ev_in, then k_merge(s)      -> ev_m[p]
+ *   ms:      wait ev_d[s%2] (implies ev_in), then k_merge(s) -> ev_m[p]
  *   caller:  wait ev_m[(s-2)%4] (step s-2 has finished reading its block);
  *            exact-integer contractions (int8 / fp16: k_merge never reads
  *            block rows) wait ev_ds[(s-2)%4], k_dist_topk(s-2) alone, so
@@ -871,6 +880,14 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
      * block rows in k_merge) -- half the merges, which at P = 8 cost about
      * as much as the contraction. */
     const int can_pair = (c->h16 || c->i8) && 2 * c->lpq * nsplit + 1 <= 64;
+    /* a fused step behind a pending single-block step (the direct exchange:
+     * own block, then the received ones) shares its merge when the lists fit
+     * one merge wave: the own block's merge could not run beside the fused
+     * launch anyway (every CU holds a distance workgroup; measured: the
+     * merge ran on the ~20 CUs the fused launch left idle and ended after
+     * it), so pairing drops a launch and its starved tail */
+    const int pair_fused = xb && c->pend && (set & 1) && c->lpq * (c->pend_nsplit + nsplit) + 1 <= 64 &&
+                           !env_on("KNN_NO_PAIR_FUSED");
     /* a fused step (the direct exchange's received blocks) is never paired:
      * the previous step's merge runs beside it and publishes the (k+1)-th
      * d^2 of the blocks folded so far into qthr, which the fused launch's
@@ -880,7 +897,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
      * sec.5). */
     int pairing = 0;
     if ((set & 1) && c->pend) {
-        pairing = can_pair && nsplit == c->pend_nsplit && !xb;
+        pairing = (can_pair && nsplit == c->pend_nsplit && !xb) || pair_fused;
         if (!pairing) RCHK(merge_pending(c));
     }
     {
@@ -968,14 +985,15 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
     HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
     HIPCHK(hipEventRecord(c->ev_ds[set], ds));
+    /* (the distance kernel waited for ev_in: ev_d covers the block's
+     * arrival too -- a second wait would add its own latency) */
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));
-    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_in, 0));
     if (pairing) {
         /* the pending even step's kernel signalled ev_d[ds_i ^ 1], not yet
          * re-recorded (the next record is step s+1's) */
         HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i ^ 1], 0));
         c->pend = 0;
-        RCHK(launch_merge_sets(c, c->pend_set, 2, 2 * nsplit, cblk, c_base, nc));
+        RCHK(launch_merge_sets(c, c->pend_set, 2, c->pend_nsplit + nsplit, cblk, c_base, nc));
         if (c->pend_ev) HIPCHK(hipEventRecord(c->pend_ev[2], c->ms));
         if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
     } else if (!(set & 1) && can_pair) {
@@ -1046,16 +1064,22 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     if (!c || !d_out || c->first_step) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
+    /* finalize and the counter read-back run on the merge stream right
+     * behind the last merge: every cross-stream wait (hipStreamWaitEvent)
+     * put ~20 us of latency on the pass's critical path, even when the
+     * event had long completed (rocprofv3 of the P = 8 ring emulation).
+     * d_out must not be in use by work pending on other streams (knn.h);
+     * the caller's stream is ordered after the results. */
     RCHK(merge_pending(c));
-    HIPCHK(hipStreamWaitEvent(s, c->ev_m[(c->nstep - 1) % KNN_PSETS], 0));   /* the last merge */
     RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
                              (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
                              c->fail_list, c->mode_dev, c->fbound, env_on("KNN_FORCE_RESCAN"),
-                             c->split, stream));
+                             c->split, c->ms));
     int host[2];
-    HIPCHK(hipMemcpyAsync(&host[0], c->fail_count, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&host[1], c->mode_dev, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpyAsync(host, c->fail_count, 2 * sizeof(int), hipMemcpyDeviceToHost, c->ms));
+    HIPCHK(hipEventRecord(c->ev_end, c->ms));
+    HIPCHK(hipStreamWaitEvent(s, c->ev_end, 0));
+    HIPCHK(hipStreamSynchronize(c->ms));
     RCHK(prof_collect(c));
     c->nfail = host[0];
     c->mode = host[1];

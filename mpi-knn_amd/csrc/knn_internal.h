@@ -122,6 +122,13 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
 /* fp16 shadow rows (round_up(n, 64) halves a row) of a packed block */
 int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
+/* INT-mode merge of int8 lane lists (kl = KNN_I8_KL_S / KNN_I8_KL, kp <= 64)
+ * by ranking the candidates at or below the shared bound (k_merge_rank) */
+int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const double *part_d, const int *part_i,
+                          const double *part_T, int nsplit, int lpq, int nq, int nq_pad, int first_step,
+                          double *st_d, double *st_x, int *st_i, double *st_T, double *qthr, void *stream);
+/* qthr = +inf, qsum (may be NULL) = empty summaries, counts[0..1] = 0 */
+int knn_launch_begin_init(double *qthr, unsigned long long *qsum, int nq_pad, int *counts, void *stream);
 /* split fp16 shadow rows of an fp32 / fp64 block: per 32 features 32 halves hi =
  * RN16(S x), then 32 halves lo = RN16(S x - hi); rows of round_up(n, 32) * 4
  * bytes; S a power of two (knn_engine.c: maxabs S in [2^13, 2^14)) */

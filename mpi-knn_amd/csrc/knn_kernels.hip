@@ -1211,6 +1211,136 @@ __global__ __launch_bounds__(256) void k_merge(
 }
 
 // ---------------------------------------------------------------------------
+// k_merge_rank: the INT-mode merge of int8 lane lists (k_dist_topk_i8: exact
+// integer d^2 < 2^31, zeros never admitted) by ranking instead of argmin
+// rounds.  One wave per query.  The shared bound qthr[q] is an upper bound on
+// the query's (k+1)-th smallest d^2 over all rows (k + 1 distinct rows lie at
+// or below it), so no entry above it can be among the k + 1 smallest: every
+// list entry and state entry at or below it is compacted into LDS as a u64
+// key (d^2 << 32 | idx: u64 order is the reference's (d, idx) order, SURVEY
+// F1; keys are distinct), each candidate's rank is the number of smaller
+// keys, and rank r < k + 1 goes to state slot r.  The rank of a candidate
+// costs C compares a lane (C candidates, ~31..100 at the end of a search);
+// k_merge's k + 1 dependent wave-argmin rounds cost ~2k cycles each in
+// latency (rocprofv3: 33 us for 7500 queries, 0.19 ms for 60000).
+// State, T, Td and the publication as k_merge's INT mode (the (k+1)-th of
+// the merged entries is published into qthr).
+// ---------------------------------------------------------------------------
+typedef unsigned long long knn_u64x2 __attribute__((ext_vector_type(2)));
+template <typename TE, int KP, int KL>
+__global__ __launch_bounds__(256) void k_merge_rank(
+    const double *__restrict__ part_d, const int *__restrict__ part_i, const double *__restrict__ part_T,
+    int nsplit, int lpq, int nq, int nq_pad, int first_step, double *__restrict__ st_d,
+    double *__restrict__ st_x, int *__restrict__ st_i, double *__restrict__ st_T, int k,
+    unsigned long long *__restrict__ qthr, int cap)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned long long mr_buf[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + wave;
+    if (q >= nq) return;   // wave-uniform, and no workgroup barrier below
+    LDS_AS unsigned long long *buf = (LDS_AS unsigned long long *)mr_buf + (size_t)wave * cap;
+    const int nl = lpq * nsplit;
+    // any value read is a valid bound (it only falls); floor: d^2 are integers
+    const double qb = __longlong_as_double((long long)qthr[q]);
+    const double B = qb >= 4294967295.0 ? 4294967295.0 : floor(qb);
+
+    double d[KL];
+    int id[KL];
+#pragma unroll
+    for (int e = 0; e < KL; e++) {
+        d[e] = KNN_INF;
+        id[e] = 0;
+    }
+    int c = 0;
+    if (lane < nl) {
+        const int s = lane / lpq, g = lane - s * lpq;
+        const size_t base = (((size_t)s * nq_pad + q) * lpq + g) * KL;
+        // the list is sorted: read it 4 entries at a time while the last
+        // one read is still at or below the bound (a late merge reads 1-2
+        // entries of most lists)
+#pragma unroll
+        for (int e0 = 0; e0 < KL; e0 += 4) {
+            if (e0 > 0 && !(d[e0 - 1] <= B)) break;
+#pragma unroll
+            for (int e = e0; e < e0 + 4 && e < KL; e++) {
+                d[e] = part_d[base + e];
+                id[e] = part_i[base + e];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < KL; e++) c += d[e] <= B ? 1 : 0;   // a prefix (+inf past the end)
+    }
+    double sdv = KNN_INF;
+    int siv = -1, cs = 0;
+    if (!first_step && lane < KP) {
+        sdv = st_d[(size_t)q * KP + lane];
+        siv = st_i[(size_t)q * KP + lane];
+        cs = (siv >= 0 && sdv <= B) ? 1 : 0;
+    }
+    // exclusive prefix of the per-lane counts (<= KL + 1 < 32): bit-sliced
+    // through mbcnt
+    const int ct = c + cs;
+    int pre = 0, C = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) {
+        const unsigned long long m = __ballot((ct >> b) & 1);
+        pre += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << b;
+        C += __popcll(m) << b;
+    }
+#pragma unroll
+    for (int e = 0; e < KL; e++)
+        if (e < c) buf[pre + e] = ((unsigned long long)(unsigned)d[e] << 32) | (unsigned)id[e];
+    if (cs) buf[pre + c] = ((unsigned long long)(unsigned)sdv << 32) | (unsigned)siv;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    const int kk = k + 1 < KP ? k + 1 : KP;   // entries the state keeps
+    for (int b0 = 0; b0 < C; b0 += 64) {
+        const int my = b0 + lane;
+        const unsigned long long x = my < C ? buf[my] : ~0ull;
+        int r = 0, j = 0;
+        for (; j + 4 <= C; j += 4) {   // broadcast reads, 2 keys each
+            const knn_u64x2 a = *(const LDS_AS knn_u64x2 *)(buf + j);
+            const knn_u64x2 b = *(const LDS_AS knn_u64x2 *)(buf + j + 2);
+            r += (a.x < x ? 1 : 0) + (a.y < x ? 1 : 0) + (b.x < x ? 1 : 0) + (b.y < x ? 1 : 0);
+        }
+        for (; j < C; j++) r += buf[j] < x ? 1 : 0;
+        if (my < C) {
+            const double dv = (double)(unsigned)(x >> 32);
+            if (r < kk) {
+                st_d[(size_t)q * KP + r] = dv;
+                st_x[(size_t)q * KP + r] = dv;
+                st_i[(size_t)q * KP + r] = (int)(unsigned)x;
+            }
+            if (r == k) {   // the (k+1)-th: a bound on the query's (k+1)-th over all rows
+                double u = dv;
+                if constexpr (sizeof(TE) == 4) u = (double)__double2float_ru(u);
+                atomicMin(qthr + q, (unsigned long long)__double_as_longlong(u));
+            }
+        }
+    }
+    if (lane < KP && lane >= (C < kk ? C : kk)) {
+        st_d[(size_t)q * KP + lane] = KNN_INF;
+        st_x[(size_t)q * KP + lane] = KNN_INF;
+        st_i[(size_t)q * KP + lane] = -1;
+    }
+    double T = KNN_INF, Td = KNN_INF;
+    if (lane < nsplit) T = part_T[(size_t)lane * nq_pad + q];
+    if (!first_step && lane == 63) {
+        T = fmin(T, st_T[2 * (size_t)q]);
+        Td = st_T[2 * (size_t)q + 1];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        T = fmin(T, __shfl_xor(T, off));
+        Td = fmin(Td, __shfl_xor(Td, off));
+    }
+    if (lane == 0) {
+        st_T[2 * (size_t)q] = T;
+        st_T[2 * (size_t)q + 1] = Td;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_finalize: one wave per query.  Order by (sqrt(S), idx) -- the key the
 // reference keeps (knn-serial.c:86-90) -- drop S == 0, and certify: every
 // candidate outside the state has approx d^2 >= T, hence exact S >= T - E
@@ -1553,6 +1683,29 @@ __global__ void k_fill_inf(double *p, int count)
 {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) p[i] = KNN_INF;
+}
+
+// begin(): the shared bounds (+inf), the int8 kernel's cross-split summaries
+// (0x7f7f7f7f pairs: above every int8-mode d^2) and the two counters
+// (unresolved queries, mode) in one launch instead of three
+__global__ void k_begin_init(double *qthr, unsigned long long *qsum, int nq_pad, int *counts)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nq_pad) qthr[i] = KNN_INF;
+    if (qsum != nullptr && i < nq_pad) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) qsum[4 * (size_t)i + j] = 0x7f7f7f7f7f7f7f7full;
+    }
+    if (i < 2) counts[i] = 0;
+}
+
+extern "C" int knn_launch_begin_init(double *qthr, unsigned long long *qsum, int nq_pad, int *counts,
+                                     void *stream)
+{
+    const int n = nq_pad > 2 ? nq_pad : 2;
+    hipLaunchKernelGGL(k_begin_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       qthr, qsum, nq_pad, counts);
+    return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
 }
 
 extern "C" int knn_launch_fill_inf(double *p, int count, void *stream)
@@ -1955,6 +2108,33 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL
+}
+
+extern "C" int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const double *part_d, const int *part_i,
+                                     const double *part_T, int nsplit, int lpq, int nq, int nq_pad,
+                                     int first_step, double *st_d, double *st_x, int *st_i, double *st_T,
+                                     double *qthr, void *stream)
+{
+    if (lpq < 1 || nsplit < 1 || lpq * nsplit > 64 || k <= 0 || k > kp || kp > 64 || nsplit > 64 ||
+        (kl != KNN_I8_KL_S && kl != KNN_I8_KL))
+        return KNN_ERR_INVALID;
+    const int cap = (lpq * nsplit * kl + kp + 1) & ~1;   // every candidate; 16-byte rows
+    const size_t lds = 4 * (size_t)cap * sizeof(unsigned long long);
+    const dim3 grid((unsigned)((nq + 3) / 4));
+    hipStream_t s = (hipStream_t)stream;
+#define RANK(T, KP, KL)                                                                            \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge_rank<T, KP, KL>), grid, dim3(256), lds, s, part_d, part_i, \
+                       part_T, nsplit, lpq, nq, nq_pad, first_step, st_d, st_x, st_i, st_T, k,       \
+                       (unsigned long long *)qthr, cap)
+    if (dtype == KNN_F64 && kp == KNN_KP && kl == KNN_I8_KL_S) RANK(double, KNN_KP, KNN_I8_KL_S);
+    else if (dtype == KNN_F64 && kp == KNN_KP) RANK(double, KNN_KP, KNN_I8_KL);
+    else if (dtype == KNN_F32 && kp == KNN_KP && kl == KNN_I8_KL_S) RANK(float, KNN_KP, KNN_I8_KL_S);
+    else if (dtype == KNN_F32 && kp == KNN_KP) RANK(float, KNN_KP, KNN_I8_KL);
+    else if (dtype == KNN_F32 && kp == KNN_KP_M && kl == KNN_I8_KL_S) RANK(float, KNN_KP_M, KNN_I8_KL_S);
+    else if (dtype == KNN_F32 && kp == KNN_KP_M) RANK(float, KNN_KP_M, KNN_I8_KL);
+    else return KNN_ERR_INVALID;
+#undef RANK
+    return hip_status();
 }
 
 extern "C" int knn_launch_finalize(int dtype, int kp, const double *st_d, const double *st_x,

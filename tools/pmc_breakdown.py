@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-dispatch PMC values of the distance kernels in one rocprofv3 --pmc
+"""Per-dispatch PMC values of the distance and merge kernels in one rocprofv3 --pmc
 pass (tools/gpu.sh pmcx:WL:GROUP), with the derived ratios the kernel work
 is read by: instructions per wave, cycle buckets per wave-cycle, MFMA busy.
 
@@ -27,7 +27,7 @@ def main():
     res = {}
     for d in sys.argv[1:]:
         for (k, disp), cs in sorted(per_dispatch(d).items()):
-            if not k.startswith("k_dist_topk"):
+            if not k.startswith(("k_dist_topk", "k_merge")):
                 continue
             rec = dict(cs)
             w = cs.get("SQ_WAVES")
