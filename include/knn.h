@@ -256,6 +256,32 @@ KNN_API int knn_ctx_begin(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap, si
 KNN_API int knn_ctx_begin_meta(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap, size_t q_base,
                                const double *d_meta, const double *h_meta, void *stream);
 
+/* Speculative byte block (the int8 contraction's form) straight from the
+ * source -- the fast path for 8-bit integer data (MNIST pixels, SIFT
+ * descriptors).  Writes knn_s8_block_bytes(cap, n) bytes: rows of x - 128 as
+ * int8, the int8 kernel's norm words, and at knn_s8_block_meta_offset the
+ * block's 8 meta doubles (the same values knn_block_pack_dt computes, and
+ * word 7 = 1: after the MAX-reduction it says some block was packed this
+ * way; reduce them across blocks as usual).  The bytes are the int8 path's rows exactly
+ * when knn_s8_spec_ok(reduced meta) -- every value an integer in [0, 255]
+ * and the search int8-eligible; then knn_ctx_begin_s8 starts the search from
+ * it (no element block, no conversion; a ring moves it as the shadow block),
+ * otherwise pack the element block (knn_block_pack_dt) and knn_ctx_begin_meta.
+ * One read of the source, 1 byte written an element (replaces the pack of
+ * blk:100-109 plus the element -> byte conversion). */
+KNN_API size_t knn_s8_block_bytes(size_t cap, size_t n);
+KNN_API size_t knn_s8_block_meta_offset(size_t cap, size_t n);
+KNN_API int knn_block_pack_s8(void *d_sblock, int dtype, size_t cap, size_t rows, size_t n, const void *d_src,
+                              int src_dtype, size_t ld, int layout, void *stream);
+KNN_API int knn_s8_spec_ok(const double *h_meta, size_t n, int dtype);
+/* begin from the query block's speculative byte block (h_meta: the reduced
+ * meta, host; KNN_ERR_INVALID unless knn_s8_spec_ok).  The element block is
+ * needed only by the exact rescan: pack it and knn_ctx_attach_qblock before
+ * knn_ctx_rescan_step when knn_ctx_end reports unresolved queries. */
+KNN_API int knn_ctx_begin_s8(knn_ctx_t *ctx, const void *d_sblock, size_t q_cap, size_t q_base,
+                             const double *d_meta, const double *h_meta, void *stream);
+KNN_API int knn_ctx_attach_qblock(knn_ctx_t *ctx, const void *d_qblock, size_t q_cap);
+
 /* Fold one packed corpus block (nc rows, global ids c_base..) into the
  * running neighbour lists.  Blocks may come in any order (ring order).
  * Asynchronous and overlapped: the step's distance kernel may start while

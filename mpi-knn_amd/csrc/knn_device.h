@@ -81,4 +81,38 @@ __device__ __forceinline__ void wave_argmin(double &d, int &i)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Byte blocks (the int8 contraction, knn_i8.hip; written by k_shadow8 from an
+// element block or by k_pack8_* straight from the source, knn_kernels.hip)
+// ---------------------------------------------------------------------------
+// Row r of a byte block -> its slot in the norm array.  Tile t = r >> 7 owns
+// 512 bytes; inside, [m-block b][lane half h][j][i] holds row 32b + 8j + 4h +
+// i -- the row that accumulator register 4j + i of lane half h carries
+// (32x32 C/D map: row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)), so a lane
+// reads an m-block's 16 norms as 4 consecutive ds_read_b128.
+__device__ __forceinline__ int i8_norm_pos(int r)
+{
+    const int rr = r & 127, b = rr >> 5, w = rr & 31;
+    const int j = w >> 3, h = (w >> 2) & 1, i = w & 3;
+    return (r & ~127) + (((b * 2 + h) * 4 + j) * 4 + i);
+}
+
+// The norm word of row r is not |x'|^2 itself but the epilogue's addend
+//     K(r) = 31 - slot(r) - 32 |x'|^2,
+// slot(r) = 16 (b & 1) + 4 j + i: the row's position among the 32
+// accumulator registers of a pair of m-blocks (the lane's candidates in one
+// epilogue group), increasing with the row.  With A = q'.c' from the MFMA,
+//     v = 64 A + K = 32 (|q'|^2 - d^2) + (31 - slot)
+// orders the lane's candidates by (d^2, row) in ONE signed integer: the
+// lane's largest v is its nearest candidate, lowest row first on ties
+// (SURVEY F1), and d^2 = |q'|^2 - (v >> 5), slot = 31 - (v & 31) come back
+// out of it.  |x'|^2 = -(K >> 5).  Ranges (n <= 896 bytes, |x'| <= 128, d^2
+// <= n 255^2): |v| < 2^31, and inside one lane (one query) the values span
+// less than 32 (n 255^2 + 1) < 2^31 (i8_next).
+__device__ __forceinline__ int i8_norm_word(int r, int nrm)
+{
+    const int rr = r & 127, b = rr >> 5, w = rr & 31;
+    const int slot = 16 * (b & 1) + 4 * (w >> 3) + (w & 3);
+    return 31 - slot - 32 * nrm;
+}
 #endif

@@ -42,6 +42,7 @@ struct knn_ctx {
     void *qsh, *csh[KNN_PSETS];
     size_t qsh_bytes, csh_bytes;
     void *qs8, *cs8[KNN_PSETS];   /* byte blocks: the queries, converted corpus blocks */
+    const void *q8;               /* the query byte block the kernels read: qs8 or the caller's (begin_s8) */
     size_t qs8_bytes;
     int split;          /* this search filters with the split fp16 contraction (fp32 GEMM mode) */
     float sscale;       /* its power-of-two pre-scale S */
@@ -224,6 +225,19 @@ int knn_block_pack_dt(void *d_block, int dtype, size_t cap, size_t rows, size_t 
     if (layout == KNN_COLMAJOR ? ld < rows : (layout == KNN_ROWMAJOR ? ld < n : 1))
         return KNN_ERR_INVALID;
     return knn_launch_pack(d_block, dtype, cap, rows, n, d_src, src_dtype, ld, layout, stream);
+}
+
+size_t knn_s8_block_bytes(size_t cap, size_t n) { return knn_s8_bytes(cap, n); }
+size_t knn_s8_block_meta_offset(size_t cap, size_t n) { return knn_s8_norm_offset(cap, n) + knn_rows_pad(cap) * 4; }
+
+int knn_block_pack_s8(void *d_sblock, int dtype, size_t cap, size_t rows, size_t n, const void *d_src,
+                      int src_dtype, size_t ld, int layout, void *stream)
+{
+    if (!d_sblock || !d_src || rows == 0 || n == 0 || rows > cap || cap > 0x7fffffffULL || n > KNN_I8_MAX_N ||
+        !dtype_ok(dtype) || !dtype_ok(src_dtype))
+        return KNN_ERR_INVALID;
+    if (layout == KNN_COLMAJOR ? ld < rows : (layout == KNN_ROWMAJOR ? ld < n : 1)) return KNN_ERR_INVALID;
+    return knn_launch_pack_s8(d_sblock, dtype, cap, rows, n, d_src, src_dtype, ld, layout, stream);
 }
 
 int knn_block_pack(void *d_block, size_t cap, size_t rows, size_t n, const double *d_src,
@@ -470,6 +484,17 @@ static int knn_i8_exact(const double *meta, size_t n, int dtype)
     return (double)n * mx * mx <= 8388608.0 && (double)n * rg * rg <= 16777216.0;
 }
 
+/* the speculative byte block (x - 128) is the one the int8 path would build:
+ * int8-eligible data whose values all lie in [0, 255] (o = 128 - max(-x)+ =
+ * 128) */
+int knn_s8_spec_ok(const double *h_meta, size_t n, int dtype)
+{
+    const char *no_i8 = getenv("KNN_NO_I8");   /* the int8 path switched off (knn_ctx_begin_meta) */
+    if (no_i8 && no_i8[0] == '1') return 0;
+    return h_meta && dtype_ok(dtype) && knn_i8_exact(h_meta, n, dtype) && h_meta[KNN_META_MAXNEG] == 0.0 &&
+           h_meta[KNN_META_MAXPOS] <= 255.0;
+}
+
 static int env_on(const char *name)
 {
     const char *e = getenv(name);
@@ -502,12 +527,14 @@ static float knn_split_scale(const double *meta, size_t n, int dtype)
     return (float)ldexp(1.0, 14 - e);
 }
 
-int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_base,
-                       const double *d_meta, const double *h_meta, void *stream)
+/* d_s8: the query block as a byte block already (knn_block_pack_s8, valid by
+ * knn_s8_spec_ok); d_qblock is then NULL until knn_ctx_attach_qblock */
+static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_t q_cap, size_t q_base,
+                     const double *d_meta, const double *h_meta, void *stream)
 {
-    if (!c || !d_qblock || !d_meta || q_cap < c->nq) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     c->qblk = d_qblock;
+    c->q8 = NULL;
     c->q_base = q_base;
     c->q_rows_pad = knn_rows_pad(q_cap);
     c->meta = d_meta;
@@ -536,6 +563,7 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
             h_meta = hm;
         }
         c->i8 = !no_i8 && knn_i8_exact(h_meta, c->n, c->dtype);
+        if (d_s8 && !c->i8) return KNN_ERR_INVALID;
         c->h16 = !c->i8 && !no_h16 && knn_h16_exact(h_meta, c->n, c->dtype);
         if (!c->i8 && !c->h16 && !no_split) {
             c->sscale = knn_split_scale(h_meta, c->n, c->dtype);
@@ -550,7 +578,9 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
      * element fragments in the kernel instead) */
     c->shadow = c->i8 ? 2 : (c->h16 && !env_on("KNN_NO_SHADOW"));
-    if (c->i8) {
+    if (c->i8 && d_s8) {
+        c->q8 = d_s8;   /* the caller's byte block: no conversion */
+    } else if (c->i8) {
         const size_t need = knn_s8_bytes(q_cap, c->n);
         if (need > c->qs8_bytes) {
             HIPCHK(hipStreamSynchronize((hipStream_t)stream));
@@ -561,6 +591,7 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
             c->qs8_bytes = need;
         }
         RCHK(knn_launch_shadow8(c->qs8, d_qblock, c->dtype, c->q_rows_pad, c->n, d_meta, stream));
+        c->q8 = c->qs8;
     } else if (c->split) {
         const size_t need = c->q_rows_pad * knn_split_rs(c->n);
         if (need > c->qsp_bytes) {
@@ -591,6 +622,28 @@ int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t 
     return KNN_OK;
 }
 
+int knn_ctx_begin_meta(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_base,
+                       const double *d_meta, const double *h_meta, void *stream)
+{
+    if (!c || !d_qblock || !d_meta || q_cap < c->nq) return KNN_ERR_INVALID;
+    return ctx_begin(c, d_qblock, NULL, q_cap, q_base, d_meta, h_meta, stream);
+}
+
+int knn_ctx_begin_s8(knn_ctx_t *c, const void *d_sblock, size_t q_cap, size_t q_base, const double *d_meta,
+                     const double *h_meta, void *stream)
+{
+    if (!c || !d_sblock || !d_meta || !h_meta || q_cap < c->nq) return KNN_ERR_INVALID;
+    if (!knn_s8_spec_ok(h_meta, c->n, c->dtype) || env_on("KNN_NO_I8")) return KNN_ERR_INVALID;
+    return ctx_begin(c, NULL, d_sblock, q_cap, q_base, d_meta, h_meta, stream);
+}
+
+int knn_ctx_attach_qblock(knn_ctx_t *c, const void *d_qblock, size_t q_cap)
+{
+    if (!c || !d_qblock || knn_rows_pad(q_cap) != c->q_rows_pad) return KNN_ERR_INVALID;
+    c->qblk = d_qblock;
+    return KNN_OK;
+}
+
 int knn_ctx_begin(knn_ctx_t *c, const void *d_qblock, size_t q_cap, size_t q_base,
                   const double *d_meta, void *stream)
 {
@@ -612,9 +665,9 @@ int knn_ctx_shadow_pack(knn_ctx_t *c, void *d_sblock, const void *d_block, size_
     if (c->shadow != 2) return KNN_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
     const size_t rp = knn_rows_pad(cap);
-    if (d_block == c->qblk && rp == c->q_rows_pad && c->qs8) {
+    if (d_block == c->qblk && rp == c->q_rows_pad && c->q8) {
         /* the query block (a ring's own block): begin converted it already */
-        HIPCHK(hipMemcpyAsync(d_sblock, c->qs8, knn_s8_norm_offset(cap, c->n) + rp * 4, hipMemcpyDeviceToDevice,
+        HIPCHK(hipMemcpyAsync(d_sblock, c->q8, knn_s8_norm_offset(cap, c->n) + rp * 4, hipMemcpyDeviceToDevice,
                               (hipStream_t)stream));
     } else {
         RCHK(knn_launch_shadow8(d_sblock, d_block, c->dtype, rp, c->n, c->meta, stream));
@@ -919,7 +972,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     const void *csh = d_sblock, *cn_ptr = NULL;
     if (c->i8) {
         if (!d_sblock && d_cblock == c->qblk && knn_rows_pad(c->block_cap) == c->q_rows_pad) {
-            csh = c->qs8;   /* the query block itself (P = 1): its byte block exists */
+            csh = c->q8;   /* the query block itself (P = 1): its byte block exists */
         } else if (!d_sblock) {
             if (!c->cs8[set] && hipMalloc(&c->cs8[set], knn_s8_bytes(c->block_cap, c->n)) != hipSuccess)
                 return KNN_ERR_NOMEM;
@@ -971,7 +1024,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
             tab.base[0] = (int64_t)c_base;
             tab.nc[0] = (int)nc;
         }
-        RCHK(knn_launch_dist_i8(c->kp, c->klx, c->k, c->qs8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
+        RCHK(knn_launch_dist_i8(c->kp, c->klx, c->k, c->q8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
                                 knn_rows_pad(c->block_cap), (int)c->n, nsplit, c->part_d[set],
                                 c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr, c->qsum, ds));
     } else
@@ -1108,6 +1161,7 @@ int knn_ctx_rescan_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_
 {
     if (!c || !d_cblock || nc == 0) return KNN_ERR_INVALID;
     if (c->nfail == 0) return KNN_OK;
+    if (!c->qblk) return KNN_ERR_INVALID;   /* begin_s8: knn_ctx_attach_qblock first */
     HIPCHK(hipSetDevice(c->device));
     return knn_launch_rescan_step(c->dtype, c->kp, c->fail_list, c->nfail, c->fbound, c->qblk,
                                   d_cblock, c_base, (int)nc, (int)c->n, c->k, c->rs_d, c->rs_i,

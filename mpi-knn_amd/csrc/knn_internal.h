@@ -31,6 +31,8 @@ extern "C" {
 #define KNN_META_NONFINITE 3
 #define KNN_META_MAXPOS    4   /* max(x, 0)  */
 #define KNN_META_MAXNEG    5   /* max(-x, 0) */
+#define KNN_META_S8        7   /* 1: a speculative byte block (knn_block_pack_s8); MAX-reduced, so a
+                                * ring knows whether any rank packed one */
 
 /* engine modes (decided on device from the reduced meta) */
 #define KNN_MODE_INT  0   /* integer data: GEMM-form d^2 is exact         */
@@ -122,6 +124,9 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
 /* fp16 shadow rows (round_up(n, 64) halves a row) of a packed block */
 int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
+/* speculative byte block straight from the source (knn_block_pack_s8) */
+int knn_launch_pack_s8(void *dst, int dtype, size_t cap, size_t rows, size_t n, const void *src, int src_dtype,
+                       size_t ld, int layout, void *stream);
 /* INT-mode merge of int8 lane lists (kl = KNN_I8_KL_S / KNN_I8_KL, kp <= 64)
  * by ranking the candidates at or below the shared bound (k_merge_rank) */
 int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const double *part_d, const int *part_i,

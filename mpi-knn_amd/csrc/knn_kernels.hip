@@ -217,10 +217,11 @@ struct knn_meta_acc {
     }
 };
 
-// workgroup reduction of the 6 meta words (256 threads) + atomicMax
-__device__ __forceinline__ void knn_meta_flush(const knn_meta_acc &a, double mnorm, double *meta)
+// workgroup reduction of the 6 meta words (64 W threads) + atomicMax
+template <int W>
+__device__ __forceinline__ void knn_meta_flush_w(const knn_meta_acc &a, double mnorm, double *meta)
 {
-    __shared__ double red[4][6];
+    __shared__ double red[W][6];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double w[6] = {a.mabs, mnorm, a.nonint, a.nonfin, a.mpos, a.mneg};
 #pragma unroll
@@ -232,11 +233,16 @@ __device__ __forceinline__ void knn_meta_flush(const knn_meta_acc &a, double mno
     }
     __syncthreads();
     if (threadIdx.x < 6) {
-        double v = fmax(fmax(red[0][threadIdx.x], red[1][threadIdx.x]),
-                        fmax(red[2][threadIdx.x], red[3][threadIdx.x]));
+        double v = red[0][threadIdx.x];
+#pragma unroll
+        for (int x = 1; x < W; x++) v = fmax(v, red[x][threadIdx.x]);
         if (!(v >= 0.0)) v = __builtin_inf();   // NaN norm -> treat as overflow
         atomicMax((unsigned long long *)&meta[threadIdx.x], (unsigned long long)__double_as_longlong(v));
     }
+}
+__device__ __forceinline__ void knn_meta_flush(const knn_meta_acc &a, double mnorm, double *meta)
+{
+    knn_meta_flush_w<4>(a, mnorm, meta);
 }
 
 // Column-major source (the .mat layout): a workgroup owns 64 rows and walks
@@ -282,6 +288,137 @@ __global__ __launch_bounds__(256) void k_pack_col(T *__restrict__ blk, size_t ro
         else ma.nonfin = 1.0;
     }
     knn_meta_flush(ma, mnorm, meta);
+}
+
+// ---------------------------------------------------------------------------
+// Speculative byte block straight from the source (knn_block_pack_s8): the
+// int8 contraction's rows x' = x - 128 (rows of rs = round_up(n, 32) bytes,
+// zero past n and on padding rows), its norm words (i8_norm_word of the
+// exact int32 |x'|^2) and the block meta of the element pack above (the same
+// six words over the values as T).  The shift the int8 path uses is
+// o = 128 - max(-x)+ of the reduced meta (knn_i8.hip), so the image is the
+// one k_shadow8 would write exactly when every value is an integer in
+// [0, 255] -- knn_s8_spec_ok on the reduced meta (MNIST pixels, SIFT
+// descriptors); otherwise the caller packs the element block after all.  One
+// read of the source and 1 byte written an element, instead of the element
+// block (8 or 4 bytes written, read back by k_shadow8).
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ int knn_spec8(T v)
+{
+    // x - 128 of an in-window integer; anything else gives garbage the meta
+    // rejects (clamped: no undefined conversion)
+    const T c = v < (T)-1e6 ? (T)-1e6 : (v > (T)1e6 ? (T)1e6 : v);
+    return (int)c - 128;
+}
+
+// col-major source (the .mat layout): a workgroup owns 64 rows and walks the
+// columns in 64 x 64 tiles (each wave reads 64 consecutive rows of a column:
+// 512-byte runs), all 16 loads of a thread's tile in flight before their
+// conversion; bytes go through LDS into 16-byte row stores.  Thread (ty, tx)
+// sums row tx's squares over columns = ty mod 4; four partials a row.
+template <typename T, typename S>
+__global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst, size_t rows, size_t rows_pad,
+                                                   int n, int rs, const S *__restrict__ src, size_t ld)
+{
+    __shared__ unsigned char tb[64][68];   // [column of the tile][row]
+    __shared__ double part[4][64];
+    __shared__ unsigned ipart[4][64];
+    int *norms = (int *)(dst + rows_pad * (size_t)rs);
+    double *meta = (double *)(norms + rows_pad);
+    const size_t i0 = (size_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const size_t i = i0 + tx;
+    const bool live = i < rows;
+    const S *xp = src + (live ? i : 0);
+    knn_meta_acc ma;
+    double s = 0.0;
+    unsigned si = 0u;
+    for (int j0 = 0; j0 < rs; j0 += 64) {
+        S v[16];
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            const int j = j0 + ty + 4 * e;
+            v[e] = (live && j < n) ? __builtin_nontemporal_load(xp + (size_t)j * ld) : (S)0;
+        }
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            const T x = (T)v[e];
+            ma.add((double)x, s);
+            const int xi = (live && j0 + ty + 4 * e < n) ? knn_spec8(x) : 0;
+            si += (unsigned)(xi * xi);
+            tb[ty + 4 * e][tx] = (unsigned char)xi;
+        }
+        __syncthreads();
+        // row r = t / 4: 16 bytes at column 16 (t % 4) of the tile
+        const int r = threadIdx.x >> 2, c0 = 16 * (threadIdx.x & 3);
+        if (i0 + r < rows_pad && j0 + c0 < rs) {
+            unsigned w4[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                w4[q] = (unsigned)tb[c0 + 4 * q][r] | ((unsigned)tb[c0 + 4 * q + 1][r] << 8) |
+                        ((unsigned)tb[c0 + 4 * q + 2][r] << 16) | ((unsigned)tb[c0 + 4 * q + 3][r] << 24);
+            *(knn_v4i *)(dst + (i0 + r) * (size_t)rs + j0 + c0) = (knn_v4i){(int)w4[0], (int)w4[1], (int)w4[2], (int)w4[3]};
+        }
+        __syncthreads();
+    }
+    part[ty][tx] = s;
+    ipart[ty][tx] = si;
+    __syncthreads();
+    double mnorm = 0.0;
+    if (ty == 0 && i < rows_pad) {
+        const double nr = (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]);
+        const unsigned ni = (ipart[0][tx] + ipart[1][tx]) + (ipart[2][tx] + ipart[3][tx]);
+        norms[i8_norm_pos((int)i)] = i8_norm_word((int)i, (int)ni);
+        if (nr == nr) mnorm = nr;
+        else ma.nonfin = 1.0;
+    }
+    knn_meta_flush(ma, mnorm, meta);
+    if (blockIdx.x == 0 && threadIdx.x == 0) meta[KNN_META_S8] = 1.0;
+}
+
+// row-major source: one wave per row, lane l converts the 8-element groups
+// l, l + 64, ... (one 8-byte store each)
+template <typename T, typename S>
+__global__ __launch_bounds__(256) void k_pack8_row(signed char *__restrict__ dst, size_t rows, size_t rows_pad,
+                                                   int n, int rs, const S *__restrict__ src, size_t ld)
+{
+    int *norms = (int *)(dst + rows_pad * (size_t)rs);
+    double *meta = (double *)(norms + rows_pad);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ng = rs / 8;
+    knn_meta_acc ma;
+    double mnorm = 0.0;
+    for (size_t r = (size_t)blockIdx.x * 4 + wave; r < rows_pad; r += (size_t)gridDim.x * 4) {
+        double s = 0.0;
+        unsigned si = 0u;
+        const S *x = src + r * ld;
+        for (int g = lane; g < ng; g += 64) {
+            unsigned lo = 0u, hi = 0u;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const int j = 8 * g + e;
+                const bool in = r < rows && j < n;
+                const T v = in ? (T)x[j] : (T)0;
+                ma.add((double)v, s);
+                const int xi = in ? knn_spec8(v) : 0;
+                si += (unsigned)(xi * xi);
+                if (e < 4) lo |= ((unsigned)xi & 0xffu) << (8 * e);
+                else hi |= ((unsigned)xi & 0xffu) << (8 * (e - 4));
+            }
+            typedef unsigned u2 __attribute__((ext_vector_type(2)));
+            *(u2 *)(dst + r * (size_t)rs + 8 * g) = (u2){lo, hi};
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            s += __shfl_xor(s, off);
+            si += (unsigned)__shfl_xor((int)si, off);
+        }
+        if (lane == 0) norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, (int)si);
+        if (s == s) mnorm = s > mnorm ? s : mnorm;
+        else ma.nonfin = 1.0;
+    }
+    knn_meta_flush(ma, mnorm, meta);
+    if (blockIdx.x == 0 && threadIdx.x == 0) meta[KNN_META_S8] = 1.0;
 }
 
 // Row-major source: one wave per row (lane-strided features, butterfly sum).
@@ -1811,6 +1948,36 @@ static int launch_pack(T *blk, size_t cap, size_t rows, size_t n, const S *src, 
     return hip_status();
 }
 
+template <typename T, typename S>
+static int launch_pack8(signed char *dst, size_t cap, size_t rows, size_t n, const S *src, size_t ld, int layout,
+                        hipStream_t s)
+{
+    const size_t rp = knn_rows_pad(cap), rs = knn_s8_rs(n);
+    double *meta = (double *)(dst + knn_s8_norm_offset(cap, n) + rp * 4);
+    if (hipMemsetAsync(meta, 0, KNN_META_DOUBLES * sizeof(double), s) != hipSuccess) return KNN_ERR_HIP;
+    if (layout == KNN_COLMAJOR) {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_col<T, S>), dim3((unsigned)((rp + 63) / 64)), dim3(256), 0, s,
+                           dst, rows, rp, (int)n, (int)rs, src, ld);
+    } else {
+        const unsigned nb = (unsigned)((rp + 3) / 4 < 8192 ? (rp + 3) / 4 : 8192);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_row<T, S>), dim3(nb), dim3(256), 0, s, dst, rows, rp, (int)n,
+                           (int)rs, src, ld);
+    }
+    return hip_status();
+}
+
+extern "C" int knn_launch_pack_s8(void *dst, int dtype, size_t cap, size_t rows, size_t n, const void *src,
+                                  int src_dtype, size_t ld, int layout, void *stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    signed char *d = (signed char *)dst;
+    if (dtype == KNN_F64 && src_dtype == KNN_F64) return launch_pack8<double>(d, cap, rows, n, (const double *)src, ld, layout, s);
+    if (dtype == KNN_F64 && src_dtype == KNN_F32) return launch_pack8<double>(d, cap, rows, n, (const float *)src, ld, layout, s);
+    if (dtype == KNN_F32 && src_dtype == KNN_F64) return launch_pack8<float>(d, cap, rows, n, (const double *)src, ld, layout, s);
+    if (dtype == KNN_F32 && src_dtype == KNN_F32) return launch_pack8<float>(d, cap, rows, n, (const float *)src, ld, layout, s);
+    return KNN_ERR_INVALID;
+}
+
 // Ring wire form of a packed block (knn_wire_pack / knn_wire_unpack): the
 // element array as int16 (exact for integer data with max|x| <= 32767),
 // 8 elements a thread; norms and meta travel verbatim (hipMemcpyAsync).
@@ -2149,7 +2316,8 @@ extern "C" int knn_launch_finalize(int dtype, int kp, const double *st_d, const 
     hipStream_t s = (hipStream_t)stream;
 #define CALL(T, KL, KP)                                                                        \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_finalize<T, KP>), grid, dim3(256), 0, s, st_d, st_x,   \
-                       st_i, st_T, (const T *)qblk + off, nq, n, k, meta, out, fail_count,       \
+                       st_i, st_T, qblk ? (const T *)qblk + off : nullptr, nq, n, k, meta, out,  \
+                       fail_count,                                                               \
                        fail_list, mode_out, fbound, force_fail, filt);                           \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);

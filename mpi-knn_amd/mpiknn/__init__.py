@@ -45,7 +45,9 @@ API_SYMBOLS = (
     "knn_ctx_contraction_bits", "knn_wire_bytes", "knn_wire_ok", "knn_wire_pack",
     "knn_wire_unpack", "knn_shadow_bytes", "knn_shadow_norm_offset", "knn_shadow_pack",
     "knn_ctx_shadow", "knn_ctx_step_shadow", "knn_ctx_begin_meta", "knn_ctx_shadow_bytes",
-    "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n", "knn_ctx_split",
+    "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n", "knn_ctx_split", "knn_s8_block_bytes",
+    "knn_s8_block_meta_offset", "knn_block_pack_s8", "knn_s8_spec_ok", "knn_ctx_begin_s8",
+    "knn_ctx_attach_qblock",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -119,6 +121,12 @@ def _load():
         "knn_ctx_step_shadow": ([p, p, sz, sz, p], i),
         "knn_ctx_step_shadow_n": ([p, i, pp, psz, psz, p], i),
         "knn_ctx_profile": ([p, i, ctypes.POINTER(d), ctypes.POINTER(d), ctypes.POINTER(i)], i),
+        "knn_s8_block_bytes": ([sz, sz], sz),
+        "knn_s8_block_meta_offset": ([sz, sz], sz),
+        "knn_block_pack_s8": ([p, i, sz, sz, sz, p, i, sz, i, p], i),
+        "knn_s8_spec_ok": ([p, sz, i], i),
+        "knn_ctx_begin_s8": ([p, p, sz, sz, p, p, p], i),
+        "knn_ctx_attach_qblock": ([p, p, sz], i),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -281,6 +289,26 @@ def block_pack(d_block, cap, rows, n, d_src, ld, layout, stream=0, dtype="f64", 
 _live_contexts = weakref.WeakSet()
 
 
+def s8_block_bytes(cap, n):
+    return lib.knn_s8_block_bytes(cap, n)
+
+
+def s8_block_meta_offset(cap, n):
+    return lib.knn_s8_block_meta_offset(cap, n)
+
+
+def block_pack_s8(d_sblock, cap, rows, n, d_src, ld, layout, stream=0, dtype="f64", src_dtype="f64"):
+    """knn_block_pack_s8: the speculative byte block (x - 128) + meta straight
+    from the source (valid for the search iff s8_spec_ok(reduced meta))."""
+    _check(lib.knn_block_pack_s8(d_sblock, DTYPES[dtype], cap, rows, n, d_src, DTYPES[src_dtype], ld, layout,
+                                 stream or None), "knn_block_pack_s8")
+
+
+def s8_spec_ok(meta_host, n, dtype="f64"):
+    m = np.ascontiguousarray(meta_host, dtype=np.float64)
+    return bool(lib.knn_s8_spec_ok(_ptr(m), n, DTYPES[dtype]))
+
+
 @atexit.register
 def _close_all():
     # release device buffers while the HIP runtime is still up (its own
@@ -318,6 +346,15 @@ class Context:
             hm = np.ascontiguousarray(h_meta, dtype=np.float64)
             _check(lib.knn_ctx_begin_meta(self._h, d_qblock, q_cap, q_base, d_meta, _ptr(hm),
                                           stream or None), "knn_ctx_begin_meta")
+
+    def begin_s8(self, d_sblock, q_cap, q_base, d_meta, h_meta, stream=0):
+        """knn_ctx_begin_s8: start from the query block's speculative byte block"""
+        hm = np.ascontiguousarray(h_meta, dtype=np.float64)
+        _check(lib.knn_ctx_begin_s8(self._h, d_sblock, q_cap, q_base, d_meta, _ptr(hm), stream or None),
+               "knn_ctx_begin_s8")
+
+    def attach_qblock(self, d_qblock, q_cap):
+        _check(lib.knn_ctx_attach_qblock(self._h, d_qblock, q_cap), "knn_ctx_attach_qblock")
 
     def step(self, d_cblock, nc, c_base, stream=0):
         _check(lib.knn_ctx_step(self._h, d_cblock, nc, c_base, stream or None), "knn_ctx_step")

@@ -63,36 +63,71 @@ class GpuEngine:
                         for _ in range(mpiknn.STEP_LAG + 2))
         self._wires = None
         self.meta_off = mpiknn.block_meta_offset(R, n, dtype)
-        self.meta = torch.zeros(mpiknn.META_DOUBLES, dtype=torch.float64, device=self.dev)
+        self.meta = self._meta_own = torch.zeros(mpiknn.META_DOUBLES, dtype=torch.float64, device=self.dev)
         self.out = torch.zeros(max(nq, 1) * k * 16, dtype=torch.uint8, device=self.dev)
         self.ctx = mpiknn.Context(device, max(nq, 1), n, R, k, dtype)
+        # the speculative byte block (knn_block_pack_s8): tried while the
+        # data keeps qualifying (n within the int8 kernel's reach)
+        import os
+        self.try_s8 = n <= 896 and os.environ.get("KNN_NO_S8", "0") != "1"
+        self.spec = False
+        self._src = None
+        self.sq = None
 
     def stream(self):
         return self.torch.cuda.current_stream(self.dev).cuda_stream
 
-    def pack(self, src, layout_col):
+    def pack(self, src, layout_col, elements=False):
         """src: this rank's rows on the device, (rows, n) float64 or float32
-        (any strides matching the layout: col-major -> src.t() contiguous)."""
+        (any strides matching the layout: col-major -> src.t() contiguous).
+        8-bit integer data: the speculative byte block straight from src
+        (self.spec; meta word 7 = 1), else / elements=True the element block."""
         rows = src.shape[0]
+        self._src = (src, layout_col)
+        self.spec = False
+        if rows > 0 and self.try_s8 and not elements:
+            if self.sq is None:
+                self.sq = self.torch.empty(self.mk.s8_block_bytes(self.R, self.n), dtype=self.torch.uint8,
+                                           device=self.dev)
+            ld, lay, sdt = self._layout(src, layout_col)
+            self.mk.block_pack_s8(self.sq.data_ptr(), self.R, rows, self.n, src.data_ptr(), ld, lay, self.stream(),
+                                  dtype=self.dtype, src_dtype=sdt)
+            # the meta the search and the ring reduce: the byte block's own
+            # words (a view: no copy)
+            mo = self.mk.s8_block_meta_offset(self.R, self.n)
+            self.meta = self.sq[mo:mo + 8 * self.mk.META_DOUBLES].view(self.torch.float64)
+            self.spec = True
+            return
+        self.meta = self._meta_own
         if rows == 0:
             # a rank past the last row (m < P * ceil(m/P) - R): no queries,
             # an empty block; meta 0 is neutral for the MAX all-reduce
             self.qb.zero_()
             self.meta.zero_()
             return
-        if layout_col:
-            assert src.stride(0) == 1
-            ld = src.stride(1)
-            lay = self.mk.COLMAJOR
-        else:
-            assert src.stride(1) == 1
-            ld = src.stride(0)
-            lay = self.mk.ROWMAJOR
-        sdt = "f32" if src.dtype == self.torch.float32 else "f64"
+        ld, lay, sdt = self._layout(src, layout_col)
         self.mk.block_pack(self.qb.data_ptr(), self.R, rows, self.n, src.data_ptr(), ld, lay,
                            self.stream(), dtype=self.dtype, src_dtype=sdt)
         self.meta.copy_(self.qb[self.meta_off:self.meta_off + 8 * self.mk.META_DOUBLES]
                         .view(self.torch.float64))
+
+    def _layout(self, src, layout_col):
+        if layout_col:
+            assert src.stride(0) == 1
+            return src.stride(1), self.mk.COLMAJOR, ("f32" if src.dtype == self.torch.float32 else "f64")
+        assert src.stride(1) == 1
+        return src.stride(0), self.mk.ROWMAJOR, ("f32" if src.dtype == self.torch.float32 else "f64")
+
+    def pack_elements(self):
+        """the element block of the last pack's source into qb (the exact
+        rescan reads it; the reduced meta in self.meta is left as it is)"""
+        src, layout_col = self._src
+        if src.shape[0] == 0:
+            self.qb.zero_()
+            return
+        ld, lay, sdt = self._layout(src, layout_col)
+        self.mk.block_pack(self.qb.data_ptr(), self.R, src.shape[0], self.n, src.data_ptr(), ld, lay,
+                           self.stream(), dtype=self.dtype, src_dtype=sdt)
 
     def wires(self, count=3):
         """own wire block + wire receive buffers (at least `count` in all,
@@ -121,15 +156,27 @@ class GpuEngine:
                             self.stream())
 
     def begin(self, q_base, h_meta=None):
+        if self.spec:
+            self.ctx.begin_s8(self.sq.data_ptr(), self.R, q_base, self.meta.data_ptr(), h_meta, self.stream())
+            return
         self.ctx.begin(self.qb.data_ptr(), self.R, q_base, self.meta.data_ptr(), self.stream(),
                        h_meta=h_meta)
+
+    def attach_elements(self):
+        """before an exact rescan of a search begun from the byte block"""
+        if self.spec:
+            self.pack_elements()
+            self.ctx.attach_qblock(self.qb.data_ptr(), self.R)
 
     def shadow_bytes(self):
         return self.ctx.shadow_bytes(self.R)
 
     def shadow_block(self):
         """own shadow block in the search's form (knn_ctx_shadow_pack of the
-        packed own block: fp16 rows or the int8 byte block)"""
+        packed own block: fp16 rows or the int8 byte block; the speculative
+        byte block itself when the search began from it)"""
+        if self.spec:
+            return self.sq
         sb = self.ctx.shadow_bytes(self.R)
         if getattr(self, "_sqb", None) is None or self._sqb.numel() != sb:
             self._sqb = self.torch.empty(sb, dtype=self.torch.uint8, device=self.dev)
@@ -187,10 +234,29 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
     if P > 1:
         dist.all_reduce(engine.meta, op=dist.ReduceOp.MAX)
         h_meta = engine.meta.cpu().numpy()   # the ring needs it on the host anyway
+    spec = getattr(engine, "spec", False)
+    if h_meta is None and spec:
+        h_meta = engine.meta.cpu().numpy()   # (P = 1: begin would read it back anyway)
+    if h_meta is not None and h_meta[7] != 0.0 and not engine.mk.s8_spec_ok(h_meta, engine.n, engine.dtype):
+        # some rank packed the speculative byte block (meta word 7) and the
+        # reduced meta rejects it: every rank packs its element block and
+        # the meta is reduced again (the decision is the same on every rank)
+        if spec:
+            engine.pack(engine._src[0], engine._src[1], elements=True)
+            engine.try_s8 = False   # this data does not qualify: straight to elements next time
+        spec = False
+        if P > 1:
+            dist.all_reduce(engine.meta, op=dist.ReduceOp.MAX)
+            h_meta = engine.meta.cpu().numpy()
+        else:
+            h_meta = None
+    if P > 1:
         wire = (os.environ.get("KNN_NO_WIRE", "0") != "1" and hasattr(engine, "wires") and
                 engine.mk.wire_ok(h_meta))
     engine.begin(q_base, h_meta=h_meta)
-    shadow = (P > 1 and hasattr(engine, "step_shadow") and engine.ctx.shadow() != 0 and
+    # byte / fp16 shadow blocks are what the steps fold (and the ring moves);
+    # at P = 1 only a search begun from the byte block folds it explicitly
+    shadow = ((P > 1 or spec) and hasattr(engine, "step_shadow") and engine.ctx.shadow() != 0 and
               os.environ.get("KNN_NO_SHADOW_RING", "0") != "1")
 
     rx = engine.rx
@@ -315,6 +381,8 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
         t = torch.tensor([float(unresolved)], dtype=torch.float64, device=engine.meta.device)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         total = int(t.item())
+    if total > 0 and spec:
+        engine.attach_elements()   # the exact rescan reads element blocks
     if total > 0 and schedule == "direct":
         # element blocks still resident unless the pass moved shadow blocks
         direct_pass(True, held)

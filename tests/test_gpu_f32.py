@@ -30,7 +30,7 @@ def run_engine(X, k, dtype="f32"):
     m, n = X.shape
     dev = torch.device("cuda", 0)
     e = ring.GpuEngine(torch, 0, n, m, m, k, dtype=dtype)
-    e.pack(torch.from_numpy(np.ascontiguousarray(X)).to(dev), layout_col=False)
+    e.pack(torch.from_numpy(np.ascontiguousarray(X)).to(dev), layout_col=False, elements=True)
     e.begin(0)
     e.step(e.qb, m, 0)
     u = e.end()
@@ -172,7 +172,7 @@ def test_f32_ring_blocks(knn, oracle, k):
     for g in range(P):
         base, rows = blocks[g]
         e = ring.GpuEngine(torch, 0, n, R, rows, k, dtype="f32")
-        e.pack(Xd[base:base + rows].float(), layout_col=False)   # fp32 source
+        e.pack(Xd[base:base + rows].float(), layout_col=False, elements=True)   # fp32 source
         engines.append(e)
     meta = torch.stack([e.meta for e in engines]).max(dim=0).values
     for g, e in enumerate(engines):
@@ -201,7 +201,8 @@ def _split_case(X, k, monkeypatch, oracle):
     import mpiknn.ring as ring
     m, n = X.shape
     e = ring.GpuEngine(torch, 0, n, m, m, k, dtype="f32")
-    e.pack(torch.from_numpy(np.ascontiguousarray(X.astype(np.float32))).to("cuda:0"), layout_col=False)
+    e.pack(torch.from_numpy(np.ascontiguousarray(X.astype(np.float32))).to("cuda:0"), layout_col=False,
+           elements=True)
     e.begin(0)
     assert e.ctx.split() == 1, "expected the split fp16 filter"
     got, _, u = run_engine(X.astype(np.float32), k)
@@ -259,7 +260,7 @@ def test_split_filter_fp64_blocks(knn, oracle, monkeypatch, m, n):
     import torch
     import mpiknn.ring as ring
     e = ring.GpuEngine(torch, 0, n, m, m, 30, dtype="f64")
-    e.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
+    e.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False, elements=True)
     e.begin(0)
     assert e.ctx.split() == 1
     got, _, u = run_engine(X, 30, dtype="f64")

@@ -140,7 +140,7 @@ def test_ring_blocks_match_single_device(knn, oracle):
             for g in range(P):
                 base, rows = blocks[g]
                 e = ring.GpuEngine(torch, 0, n, R, rows, 30)
-                e.pack(Xd[base:base + rows], layout_col=False)
+                e.pack(Xd[base:base + rows], layout_col=False, elements=True)
                 engines.append(e)
             meta = torch.stack([e.meta for e in engines]).max(dim=0).values
             for g, e in enumerate(engines):

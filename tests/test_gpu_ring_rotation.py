@@ -111,7 +111,7 @@ def test_ring_search_rotation(knn, oracle, P, kind, schedule, monkeypatch):
     for g in range(P):
         base, rows = blocks[g]
         e = ring.GpuEngine(torch, 0, n, R, rows, 30)
-        e.pack(Xd[base:base + rows], layout_col=False)
+        e.pack(Xd[base:base + rows], layout_col=False, elements=True)
         engines.append(e)
     packed = [e.qb.clone() for e in engines]
     metas = torch.stack([e.meta for e in engines])
@@ -142,7 +142,7 @@ def test_wire_round_trip(knn, dtype):
     m, n = X.shape
     e = ring.GpuEngine(torch, 0, n, m, m, 8, dtype=dtype)
     e.pack(torch.from_numpy(X if dtype == "f64" else X.astype(np.float32)).to("cuda:0"),
-           layout_col=False)
+           layout_col=False, elements=True)
     assert knn.wire_ok(e.meta.cpu().numpy())
     w = torch.empty(knn.wire_bytes(m, n, dtype), dtype=torch.uint8, device="cuda:0")
     back = torch.empty_like(e.qb)
@@ -179,7 +179,7 @@ def test_ring_search_fp32_configs(knn, oracle, P, shape, schedule):
     for g in range(P):
         base, rows = blocks[g]
         e = ring.GpuEngine(torch, 0, n, R, rows, k, dtype="f32")
-        e.pack(Xd[base:base + rows], layout_col=False)
+        e.pack(Xd[base:base + rows], layout_col=False, elements=True)
         engines.append(e)
     packed = [e.qb.clone() for e in engines]
     metas = torch.stack([e.meta for e in engines])
@@ -216,7 +216,7 @@ def test_direct_fused_many_blocks(knn, oracle, P, fuse, monkeypatch):
     for g in range(P):
         base, rows = blocks[g]
         e = ring.GpuEngine(torch, 0, n, R, rows, 30)
-        e.pack(Xd[base:base + rows], layout_col=False)
+        e.pack(Xd[base:base + rows], layout_col=False, elements=True)
         engines.append(e)
     packed = [e.qb.clone() for e in engines]
     metas = torch.stack([e.meta for e in engines])

@@ -1,0 +1,177 @@
+"""The speculative byte block (knn_block_pack_s8): the int8 contraction's
+query/corpus rows x - 128, norm words and block meta straight from the
+source, in one pass (replaces the pack of blk:100-109 plus the element ->
+byte conversion for 8-bit integer data).
+
+* byte for byte the block k_shadow8 builds from the element block (rows and
+  norm words), with the element pack's meta (words 0-5) and word 7 = 1, for
+  col-major fp64 (the .mat layout), row-major fp64 and fp32 sources;
+* mpiknn.ring.ring_search (bench.py's per-rank code) begun from it at P = 1,
+  2 and 8 (loopback transport, both schedules) equals the oracle's scan of
+  knn-serial.c:72-93 on every rank, with and without a forced exact rescan
+  (which packs the element block after the pass);
+* data it cannot hold (a negative value, real values, values above 255)
+  falls back to the element block, still exact.
+"""
+import numpy as np
+import pytest
+
+import datasets
+from test_gpu_ring_rotation import loopback_dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("src", ["col-f64", "row-f64", "row-f32"])
+def test_s8_block_equals_shadow8(knn, src):
+    import torch
+    import mpiknn.ring as ring
+    dt = "f32" if src.endswith("f32") else "f64"
+    # fp32 INT mode needs n max^2 <= 2^23 (knn_i8_exact): 128 features
+    X = datasets.mnist_like(1000, 128 if dt == "f32" else 300, seed=3)[0]
+    X[5] = 0.0
+    X[7] = 255.0
+    m, n = X.shape
+    Xs = X.astype(np.float32) if dt == "f32" else X
+    if src.startswith("col"):
+        Xd = torch.from_numpy(np.ascontiguousarray(Xs.T)).to("cuda:0").t()
+    else:
+        Xd = torch.from_numpy(np.ascontiguousarray(Xs)).to("cuda:0")
+    ref = ring.GpuEngine(torch, 0, n, m, m, 30, dtype=dt)
+    ref.pack(Xd, layout_col=src.startswith("col"), elements=True)
+    e = ring.GpuEngine(torch, 0, n, m, m, 30, dtype=dt)
+    e.pack(Xd, layout_col=src.startswith("col"))
+    assert e.spec
+    hm = e.meta.cpu().numpy()
+    assert knn.s8_spec_ok(hm, n, dt) and hm[7] == 1.0
+    assert np.array_equal(hm[:6], ref.meta.cpu().numpy()[:6])
+    ref.begin(0, h_meta=ref.meta.cpu().numpy())
+    assert ref.ctx.shadow() == 2
+    sb = ref.shadow_block()
+    torch.cuda.synchronize()
+    # real rows (padding rows are masked by index in every kernel; k_shadow8
+    # converts their zeros, the direct pack leaves zeros)
+    rs = (n + 31) // 32 * 32
+    a, b = sb.cpu().numpy(), e.sq.cpu().numpy()
+    assert np.array_equal(a[:m * rs], b[:m * rs]), "byte rows differ from k_shadow8's"
+    rp = (m + 127) // 128 * 128
+    r = np.arange(m)
+    rr, w = r & 127, r & 31
+    pos = (r & ~127) + (((rr >> 5) * 2 + ((w >> 2) & 1)) * 4 + (w >> 3)) * 4 + (w & 3)
+    na = a[rp * rs:rp * rs + 4 * rp].view(np.int32)
+    nb = b[rp * rs:rp * rs + 4 * rp].view(np.int32)
+    assert np.array_equal(na[pos], nb[pos]), "norm words differ from k_shadow8's"
+
+
+def _engines(torch, ring, knn, X, P, k=30, dtype="f64"):
+    m, n = X.shape
+    dev = torch.device("cuda", 0)
+    Xs = X.astype(np.float32) if dtype == "f32" else X
+    Xd = torch.from_numpy(np.ascontiguousarray(Xs)).to(dev)
+    R, blocks = ring.partition(m, P)
+    engines, packed, emetas = [], [], []
+    for g in range(P):
+        base, rows = blocks[g]
+        el = ring.GpuEngine(torch, 0, n, R, rows, k, dtype=dtype)
+        el.pack(Xd[base:base + rows], layout_col=False, elements=True)
+        packed.append(el.qb.clone())
+        emetas.append(el.meta.clone())
+        e = ring.GpuEngine(torch, 0, n, R, rows, k, dtype=dtype)
+        e.pack(Xd[base:base + rows], layout_col=False)
+        engines.append(e)
+    metas = torch.stack([e.meta for e in engines])
+    wires = []
+    for el_b in packed:
+        w = torch.empty(knn.wire_bytes(R, n, dtype), dtype=torch.uint8, device=dev)
+        knn.wire_pack(w.data_ptr(), el_b.data_ptr(), R, n, dtype, engines[0].stream())
+        wires.append(w)
+    return R, blocks, engines, packed, metas, wires, torch.stack(emetas)
+
+
+def _dist(torch, g, P, packed, metas, wires, e, schedule, emetas):
+    """loopback_dist whose second meta all-reduce (after a fallback to
+    element blocks) reduces the element packs' metas"""
+    d = loopback_dist(torch, g, P, packed, metas, wires, e, schedule)
+    calls = {"n": 0}
+
+    def all_reduce(t, op):
+        if op == "max" and t.numel() == metas.shape[1]:
+            t.copy_((metas if calls["n"] == 0 else emetas).max(dim=0).values)
+            calls["n"] += 1
+    d.all_reduce = all_reduce
+    return d
+
+
+@pytest.mark.parametrize("rescan", [False, True])
+@pytest.mark.parametrize("schedule", ["direct", "ring"])
+@pytest.mark.parametrize("P", [1, 2, 8])
+def test_ring_search_from_s8(knn, oracle, P, schedule, rescan, monkeypatch):
+    """(the loopback models one continuous rotation: the neighbour ring's
+    second rotation for a rescan is covered under gloo, test_ring_cpu.py)"""
+    import torch
+    import mpiknn.ring as ring
+    if rescan and schedule == "ring" and P > 1:
+        pytest.skip("loopback hop model: one rotation")
+    if rescan:
+        monkeypatch.setenv("KNN_FORCE_RESCAN", "1")
+    X = datasets.mnist_like(2400, 784, seed=9)[0]
+    X[2000] = X[11]                                   # a duplicate across blocks
+    m, n = X.shape
+    R, blocks, engines, packed, metas, wires, emetas = _engines(torch, ring, knn, X, P)
+    for g in sorted({0, P // 2, P - 1}):
+        e = engines[g]
+        base, rows = blocks[g]
+        assert e.spec
+        d = _dist(torch, g, P, packed, metas, wires, e, schedule, emetas) if P > 1 else None
+        ring.ring_search(d, torch, e, g, P, m, base, schedule=schedule)
+        assert e.spec and e.ctx.shadow() == 2
+        got = e.result()
+        ref = oracle.knn(X, 30, rows=(base, rows))
+        assert np.array_equal(got["idx"], ref["idx"]), (P, g)
+        assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), (P, g)
+
+
+def test_ring_search_from_s8_f32_sift(knn, oracle):
+    """configs[3]'s form: fp32 rows, k = 32, P = 1 and 4"""
+    import torch
+    import mpiknn.ring as ring
+    X = datasets.sift_like(3000, 128, clusters=64, seed=4)
+    Xr = np.ascontiguousarray(X, dtype=np.float32).astype(np.float64)
+    for P in (1, 4):
+        R, blocks, engines, packed, metas, wires, emetas = _engines(torch, ring, knn, Xr, P, k=32, dtype="f32")
+        for g in (0, P - 1):
+            e = engines[g]
+            base, rows = blocks[g]
+            d = _dist(torch, g, P, packed, metas, wires, e, "direct", emetas) if P > 1 else None
+            ring.ring_search(d, torch, e, g, P, Xr.shape[0], base, schedule="direct")
+            assert e.spec
+            got = e.result()
+            ref = oracle.knn(Xr, 32, rows=(base, rows))
+            assert np.array_equal(got["idx"], ref["idx"]), (P, g)
+            assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), (P, g)
+
+
+@pytest.mark.parametrize("kind", ["negative", "real", "above255"])
+@pytest.mark.parametrize("P", [1, 4])
+def test_s8_fallback(knn, oracle, P, kind):
+    import torch
+    import mpiknn.ring as ring
+    X = datasets.mnist_like(1600, 196, seed=2)[0]
+    if kind == "negative":
+        X[P * 100 + 3, 7] = -1.0          # one value below 0 (in one rank's block only)
+    elif kind == "real":
+        X = X / 255.0 + np.random.default_rng(1).normal(0, 1e-3, X.shape)
+    else:
+        X[50, 3] = 256.0
+    m, n = X.shape
+    R, blocks, engines, packed, metas, wires, emetas = _engines(torch, ring, knn, X, P)
+    for g in range(P):
+        e = engines[g]
+        base, rows = blocks[g]
+        d = _dist(torch, g, P, packed, metas, wires, e, "direct", emetas) if P > 1 else None
+        ring.ring_search(d, torch, e, g, P, m, base, schedule="direct")
+        assert not e.spec
+        got = e.result()
+        ref = oracle.knn(X, 30, rows=(base, rows))
+        assert np.array_equal(got["idx"], ref["idx"]), (kind, P, g)
+        assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), (kind, P, g)

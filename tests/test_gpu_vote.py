@@ -55,7 +55,7 @@ def test_vote_after_device_search(knn):
     m, n = X.shape
     dev = torch.device("cuda", 0)
     e = ring.GpuEngine(torch, 0, n, m, m, 100, dtype="f32")
-    e.pack(torch.from_numpy(X).to(dev), layout_col=False)
+    e.pack(torch.from_numpy(X).to(dev), layout_col=False, elements=True)
     e.begin(0)
     e.step(e.qb, m, 0)
     if e.end():

@@ -52,7 +52,7 @@ def main():
         X = np.ascontiguousarray(X[:a.m])
     m, n = X.shape
     eng = ring.GpuEngine(torch, 0, n, m, m, k, dtype=dt)
-    eng.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
+    eng.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False, elements=True)
     eng.begin(0)
     assert eng.ctx.shadow() == 2, "data not int8-eligible"
     sb = torch.empty(eng.ctx.shadow_bytes(m), dtype=torch.uint8, device="cuda:0")

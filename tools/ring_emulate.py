@@ -101,21 +101,36 @@ def main():
             mb = t[eng.meta_off:eng.meta_off + 8 * mpiknn.META_DOUBLES].view(torch.float64)
             eng.meta.copy_(torch.maximum(eng.meta, mb))   # the ring's all_reduce(MAX)
         h_meta = eng.meta.cpu().numpy()
+        # the own block as bench.py's ring has it: the speculative byte block
+        # straight from the rows when the reduced meta accepts it (8-bit
+        # integer data), else the element block
+        spec = eng.spec and mpiknn.s8_spec_ok(h_meta, n, dt)
+        if eng.spec and not spec:
+            eng.pack(Xd[0:blocks[0][1]], layout_col=False, elements=True)
+            eng.meta.copy_(torch.stack([t[eng.meta_off:eng.meta_off + 8 * mpiknn.META_DOUBLES].view(torch.float64)
+                                        for t in bufs]).max(dim=0).values)
+            h_meta = eng.meta.cpu().numpy()
 
         # what the ring moves: the search's shadow form when it has one
         eng.begin(0, h_meta=h_meta)
-        shadow = P > 1 and eng.ctx.shadow() != 0
+        shadow = (P > 1 or spec) and eng.ctx.shadow() != 0
         sbufs = []
         if shadow:
-            for t in bufs:
+            for b, t in enumerate(bufs):
+                if b == 0 and spec:
+                    sbufs.append(eng.sq)
+                    continue
                 sb = torch.empty(eng.ctx.shadow_bytes(R), dtype=torch.uint8, device=dev)
                 eng.ctx.shadow_pack(sb.data_ptr(), t.data_ptr(), R, eng.stream())
                 sbufs.append(sb)
         for b, (base, rows) in enumerate(blocks):
-            eng.step(bufs[b], rows, base)
+            if shadow:
+                eng.step_shadow(sbufs[b], rows, base)
+            else:
+                eng.step(bufs[b], rows, base)
         eng.end()
 
-        fuse = args.fuse if shadow and eng.ctx.shadow() == 2 else "none"
+        fuse = args.fuse if shadow and P > 1 and eng.ctx.shadow() == 2 else "none"
 
         def one():
             eng.begin(0, h_meta=h_meta)
