@@ -29,6 +29,10 @@
  *   KNN_I8_KL=17          17-entry int8 lane lists instead of 12
  *   KNN_SPLITS=s          corpus splits per launch instead of the model's
  *   KNN_NO_FUSE=1         fold received byte blocks one launch each
+ *   KNN_NO_PAIR_FUSED=1   the own block's step keeps a merge of its own
+ *                         instead of sharing the fused step's
+ *   KNN_NO_RANK_MERGE=1   int8 lists merged by k_merge's argmin rounds
+ *                         instead of k_merge_rank
  *   KNN_FORCE_RESCAN=1    send every query through the exact rescan pass
  *   KNN_FORCE_RING=1      knn_search runs the ring driver on one GPU
  *   KNN_RING_SCHEDULE=ring|direct
@@ -42,6 +46,8 @@
  *   KNN_RING_LOOPBACK=1   P virtual ranks on device 0 (tests)
  *   KNN_NO_SHADOW_RING=1  ring moves element blocks, not shadow/byte blocks
  *   KNN_MAT / KNN_MPI_COMPAT  the CLIs: .mat path, bug-compatible mode
+ *   (mpiknn/ring.py: KNN_NO_S8=1 packs element blocks, not the byte block
+ *   of knn_block_pack_s8)
  */
 #ifndef KNN_H
 #define KNN_H
