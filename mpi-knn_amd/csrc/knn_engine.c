@@ -65,6 +65,10 @@ struct knn_ctx {
     size_t pp_per[KNN_PSETS / 2];     /* list entries per split it was sized for */
     /* an even step whose merge waits for the next step (pairing) */
     int pend, pend_set, pend_nsplit, pend_nc, merged;
+    /* a paired merge of a fused step, deferred to the next step or to
+     * knn_ctx_end (which then merges and finalizes in one launch) */
+    int pend2, pend2_set, pend2_nsplit;
+    hipEvent_t *pend2_ev[2];
     int even_nsplit;                  /* splits of the last even step: the odd set's offset */
     const void *pend_cblk;
     size_t pend_cbase;
@@ -542,6 +546,7 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
     c->nstep = 0;
     c->pend = 0;
     c->pend_nsplit = 0;
+    c->pend2 = 0;
     c->even_nsplit = 0;
     c->merged = 0;
     c->nfail = 0;
@@ -838,35 +843,69 @@ static int ensure_part_buffers(knn_ctx_t *c, int nsplit, int set, int off)
 /* k_merge of `nsets` consecutive steps' lists (1, or 2 = a pending even
  * step and the odd step behind it) starting at set `set`, on ms after
  * their distance kernels; records ev_m of every covered set. */
-static int launch_merge_sets(knn_ctx_t *c, int set, int nsets, int nsplit_total, const void *cblk,
-                             size_t c_base, size_t nc)
+static int rank_merge_ok(const knn_ctx_t *c, int nsplit_total)
 {
+    return c->i8 && c->kp <= KNN_KP_M && (c->klx == KNN_I8_KL_S || c->klx == KNN_I8_KL) &&
+           c->lpq * nsplit_total <= 64 && !env_on("KNN_NO_RANK_MERGE");
+}
+
+/* fin_out: the search's last merge -- with the rank merge it finalizes
+ * too (records into fin_out, *finalized = 1) */
+static int launch_merge_sets_fin(knn_ctx_t *c, int set, int nsets, int nsplit_total, const void *cblk,
+                                 size_t c_base, size_t nc, knn_neighbour_t *fin_out, int *finalized)
+{
+    if (finalized) *finalized = 0;
     /* int8 lists (exact INT-mode keys, k <= 32): the rank merge */
-    if (c->i8 && c->kp <= KNN_KP_M && (c->klx == KNN_I8_KL_S || c->klx == KNN_I8_KL) &&
-        c->lpq * nsplit_total <= 64 && !env_on("KNN_NO_RANK_MERGE"))
+    if (rank_merge_ok(c, nsplit_total)) {
         RCHK(knn_launch_merge_rank(c->dtype, c->kp, c->klx, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
                                    nsplit_total, c->lpq, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d,
-                                   c->st_x, c->st_i, c->st_T, c->qthr, c->ms));
-    else
+                                   c->st_x, c->st_i, c->st_T, c->qthr, fin_out, c->fail_count, c->fail_list,
+                                   c->mode_dev, c->fbound, c->meta, (int)c->n, env_on("KNN_FORCE_RESCAN"), c->ms));
+        if (fin_out && finalized) *finalized = 1;
+    } else
         RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
                               nsplit_total, c->lpq, c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x,
                               c->st_i, c->st_T, c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n,
                               c->meta, c->qthr, c->split, c->ms));
     c->merged = 1;
-    for (int x = 0; x < nsets; x++) HIPCHK(hipEventRecord(c->ev_m[(set + x) % KNN_PSETS], c->ms));
+    /* (the search's last merge: nothing waits on its sets -- an event
+     * record is one more packet on the queue before the read-back) */
+    if (!(finalized && *finalized))
+        for (int x = 0; x < nsets; x++) HIPCHK(hipEventRecord(c->ev_m[(set + x) % KNN_PSETS], c->ms));
+    return KNN_OK;
+}
+
+static int launch_merge_sets(knn_ctx_t *c, int set, int nsets, int nsplit_total, const void *cblk,
+                             size_t c_base, size_t nc)
+{
+    return launch_merge_sets_fin(c, set, nsets, nsplit_total, cblk, c_base, nc, NULL, NULL);
+}
+
+/* the deferred merge of a fused step and its pending partner */
+static int flush_pend2(knn_ctx_t *c, knn_neighbour_t *fin_out, int *finalized)
+{
+    if (finalized) *finalized = 0;
+    if (!c->pend2) return KNN_OK;
+    c->pend2 = 0;
+    RCHK(launch_merge_sets_fin(c, c->pend2_set, 2, c->pend2_nsplit, NULL, 0, 0, fin_out, finalized));
+    for (int x = 0; x < 2; x++)
+        if (c->pend2_ev[x]) HIPCHK(hipEventRecord(c->pend2_ev[x][2], c->ms));
     return KNN_OK;
 }
 
 /* merge the pending even step by itself */
-static int merge_pending(knn_ctx_t *c)
+static int merge_pending_fin(knn_ctx_t *c, knn_neighbour_t *fin_out, int *finalized)
 {
+    if (finalized) *finalized = 0;
     if (!c->pend) return KNN_OK;
     c->pend = 0;
-    RCHK(launch_merge_sets(c, c->pend_set, 1, c->pend_nsplit, c->pend_cblk, c->pend_cbase,
-                           (size_t)c->pend_nc));
+    RCHK(launch_merge_sets_fin(c, c->pend_set, 1, c->pend_nsplit, c->pend_cblk, c->pend_cbase,
+                               (size_t)c->pend_nc, fin_out, finalized));
     if (c->pend_ev) HIPCHK(hipEventRecord(c->pend_ev[2], c->ms));
     return KNN_OK;
 }
+
+static int merge_pending(knn_ctx_t *c) { return merge_pending_fin(c, NULL, NULL); }
 
 /* Step schedule.  Step s runs k_dist_topk on stream ds[s % 2] into partial
  * set p = s % 4 and k_merge on stream ms (high priority), in step order:
@@ -925,6 +964,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     if (d_sblock && !c->shadow) return KNN_ERR_INVALID;
     if (!d_cblock) d_cblock = d_sblock;   /* INT mode: k_merge never reads its rows */
     HIPCHK(hipSetDevice(c->device));
+    RCHK(flush_pend2(c, NULL, NULL));   /* a deferred merge goes first, in step order */
     const int nsplit = choose_splits(c, nc);
     const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
     c->nsplit_last = nsplit;
@@ -1046,9 +1086,21 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
          * re-recorded (the next record is step s+1's) */
         HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i ^ 1], 0));
         c->pend = 0;
-        RCHK(launch_merge_sets(c, c->pend_set, 2, c->pend_nsplit + nsplit, cblk, c_base, nc));
-        if (c->pend_ev) HIPCHK(hipEventRecord(c->pend_ev[2], c->ms));
-        if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
+        if (xb && rank_merge_ok(c, c->pend_nsplit + nsplit)) {
+            /* the fused step (the direct exchange's last): its merge waits
+             * for the next call -- knn_ctx_end merges and finalizes in one
+             * launch (a separate k_finalize cost its launch and ~20 us of
+             * queue gap, rocprofv3) */
+            c->pend2 = 1;
+            c->pend2_set = c->pend_set;
+            c->pend2_nsplit = c->pend_nsplit + nsplit;
+            c->pend2_ev[0] = c->pend_ev;
+            c->pend2_ev[1] = ev;
+        } else {
+            RCHK(launch_merge_sets(c, c->pend_set, 2, c->pend_nsplit + nsplit, cblk, c_base, nc));
+            if (c->pend_ev) HIPCHK(hipEventRecord(c->pend_ev[2], c->ms));
+            if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
+        }
     } else if (!(set & 1) && can_pair) {
         c->pend = 1;
         c->pend_set = set;
@@ -1123,11 +1175,16 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
      * event had long completed (rocprofv3 of the P = 8 ring emulation).
      * d_out must not be in use by work pending on other streams (knn.h);
      * the caller's stream is ordered after the results. */
-    RCHK(merge_pending(c));
-    RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
-                             (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
-                             c->fail_list, c->mode_dev, c->fbound, env_on("KNN_FORCE_RESCAN"),
-                             c->split, c->ms));
+    /* the last merge (deferred or pending) finalizes too when it is the
+     * rank merge (INT-mode int8 lists) */
+    int fin = 0;
+    RCHK(flush_pend2(c, d_out, &fin));
+    if (!fin) RCHK(merge_pending_fin(c, d_out, &fin));
+    if (!fin)
+        RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
+                                 (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
+                                 c->fail_list, c->mode_dev, c->fbound, env_on("KNN_FORCE_RESCAN"),
+                                 c->split, c->ms));
     int host[2];
     HIPCHK(hipMemcpyAsync(host, c->fail_count, 2 * sizeof(int), hipMemcpyDeviceToHost, c->ms));
     HIPCHK(hipEventRecord(c->ev_end, c->ms));

@@ -131,7 +131,9 @@ int knn_launch_pack_s8(void *dst, int dtype, size_t cap, size_t rows, size_t n, 
  * by ranking the candidates at or below the shared bound (k_merge_rank) */
 int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const double *part_d, const int *part_i,
                           const double *part_T, int nsplit, int lpq, int nq, int nq_pad, int first_step,
-                          double *st_d, double *st_x, int *st_i, double *st_T, double *qthr, void *stream);
+                          double *st_d, double *st_x, int *st_i, double *st_T, double *qthr,
+                          knn_neighbour_t *fin_out, int *fail_count, int *fail_list, int *mode_out, double *fbound,
+                          const double *meta, int n, int force_fail, void *stream);
 /* qthr = +inf, qsum (may be NULL) = empty summaries, counts[0..1] = 0 */
 int knn_launch_begin_init(double *qthr, unsigned long long *qsum, int nq_pad, int *counts, void *stream);
 /* split fp16 shadow rows of an fp32 / fp64 block: per 32 features 32 halves hi =

@@ -1364,12 +1364,22 @@ __global__ __launch_bounds__(256) void k_merge(
 // the merged entries is published into qthr).
 // ---------------------------------------------------------------------------
 typedef unsigned long long knn_u64x2 __attribute__((ext_vector_type(2)));
+// fin != 0 (the search's last merge, knn_ctx_end): k_finalize's INT-mode
+// work in the same pass -- certify tau_k < T, emit the k records or put the
+// query on the rescan list -- instead of writing the state.
+struct knn_fin_args {
+    knn_neighbour_t *out;
+    int *fail_count, *fail_list, *mode_out;
+    double *fbound;
+    const double *meta;
+    int n, force_fail;
+};
 template <typename TE, int KP, int KL>
 __global__ __launch_bounds__(256) void k_merge_rank(
     const double *__restrict__ part_d, const int *__restrict__ part_i, const double *__restrict__ part_T,
     int nsplit, int lpq, int nq, int nq_pad, int first_step, double *__restrict__ st_d,
     double *__restrict__ st_x, int *__restrict__ st_i, double *__restrict__ st_T, int k,
-    unsigned long long *__restrict__ qthr, int cap)
+    unsigned long long *__restrict__ qthr, int cap, int fin, knn_fin_args fa)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned long long mr_buf[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1432,6 +1442,34 @@ __global__ __launch_bounds__(256) void k_merge_rank(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
     const int kk = k + 1 < KP ? k + 1 : KP;   // entries the state keeps
+    // T: the smallest rejection bound of the merged lanes (and the state)
+    double T = KNN_INF, Td = KNN_INF;
+    if (lane < nsplit) T = part_T[(size_t)lane * nq_pad + q];
+    if (!first_step && lane == 63) {
+        T = fmin(T, st_T[2 * (size_t)q]);
+        Td = st_T[2 * (size_t)q + 1];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        T = fmin(T, __shfl_xor(T, off));
+        Td = fmin(Td, __shfl_xor(Td, off));
+    }
+    // fin: the records are written as the ranks come out; the query is
+    // certified (or put on the rescan list, whose pass rewrites them) after
+    const bool emit = fin != 0;
+    int mode = KNN_MODE_INT;
+    if (fin) {
+        mode = knn_mode<TE>(fa.meta, fa.n);
+        if (blockIdx.x == 0 && threadIdx.x == 0) *fa.mode_out = mode;
+        // slots past the candidates: {inf, 0, 0}
+        if (lane < k && lane >= C) {
+            knn_neighbour_t rec;
+            rec.distance = KNN_INF;
+            rec.idx = 0;
+            rec.label = 0;
+            fa.out[(size_t)q * k + lane] = rec;
+        }
+    }
+    double tau = KNN_INF;   // fin: the k-th kept d^2
     for (int b0 = 0; b0 < C; b0 += 64) {
         const int my = b0 + lane;
         const unsigned long long x = my < C ? buf[my] : ~0ull;
@@ -1444,32 +1482,45 @@ __global__ __launch_bounds__(256) void k_merge_rank(
         for (; j < C; j++) r += buf[j] < x ? 1 : 0;
         if (my < C) {
             const double dv = (double)(unsigned)(x >> 32);
-            if (r < kk) {
+            if (emit) {
+                if (r < k) {
+                    knn_neighbour_t rec;
+                    rec.distance = sqrt(dv);
+                    rec.idx = (int)(unsigned)x + 1;
+                    rec.label = 0;
+                    fa.out[(size_t)q * k + r] = rec;
+                }
+            } else if (r < kk) {
                 st_d[(size_t)q * KP + r] = dv;
                 st_x[(size_t)q * KP + r] = dv;
                 st_i[(size_t)q * KP + r] = (int)(unsigned)x;
             }
-            if (r == k) {   // the (k+1)-th: a bound on the query's (k+1)-th over all rows
+            if (r == k && !emit) {   // the (k+1)-th: a bound on the query's (k+1)-th over all rows
                 double u = dv;
                 if constexpr (sizeof(TE) == 4) u = (double)__double2float_ru(u);
                 atomicMin(qthr + q, (unsigned long long)__double_as_longlong(u));
             }
         }
+        if (emit) {
+            const unsigned long long at = __ballot(my < C && r == k - 1);
+            if (at) tau = (double)(unsigned)(__shfl(x, __builtin_ctzll(at)) >> 32);
+        }
+    }
+    if (emit) {
+        // k_finalize, INT mode: zeros were never admitted, so the rank-(k-1)
+        // candidate is tau; a candidate a lane turned away has d^2 >= T, and
+        // with d^2 == T it may precede the k-th by index: certify tau < T
+        const bool ok = mode == KNN_MODE_INT && !fa.force_fail && (T == KNN_INF || (C >= k && tau < T));
+        if (!ok && lane == 0) {
+            fa.fail_list[atomicAdd(fa.fail_count, 1)] = q;
+            fa.fbound[q] = (fa.force_fail || mode != KNN_MODE_INT) ? KNN_INF : sqrt(tau);
+        }
+        return;
     }
     if (lane < KP && lane >= (C < kk ? C : kk)) {
         st_d[(size_t)q * KP + lane] = KNN_INF;
         st_x[(size_t)q * KP + lane] = KNN_INF;
         st_i[(size_t)q * KP + lane] = -1;
-    }
-    double T = KNN_INF, Td = KNN_INF;
-    if (lane < nsplit) T = part_T[(size_t)lane * nq_pad + q];
-    if (!first_step && lane == 63) {
-        T = fmin(T, st_T[2 * (size_t)q]);
-        Td = st_T[2 * (size_t)q + 1];
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        T = fmin(T, __shfl_xor(T, off));
-        Td = fmin(Td, __shfl_xor(Td, off));
     }
     if (lane == 0) {
         st_T[2 * (size_t)q] = T;
@@ -2280,8 +2331,20 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
 extern "C" int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const double *part_d, const int *part_i,
                                      const double *part_T, int nsplit, int lpq, int nq, int nq_pad,
                                      int first_step, double *st_d, double *st_x, int *st_i, double *st_T,
-                                     double *qthr, void *stream)
+                                     double *qthr, knn_neighbour_t *fin_out, int *fail_count, int *fail_list,
+                                     int *mode_out, double *fbound, const double *meta, int n, int force_fail,
+                                     void *stream)
 {
+    knn_fin_args fa;
+    fa.out = fin_out;
+    fa.fail_count = fail_count;
+    fa.fail_list = fail_list;
+    fa.mode_out = mode_out;
+    fa.fbound = fbound;
+    fa.meta = meta;
+    fa.n = n;
+    fa.force_fail = force_fail;
+    const int fin = fin_out != nullptr;
     if (lpq < 1 || nsplit < 1 || lpq * nsplit > 64 || k <= 0 || k > kp || kp > 64 || nsplit > 64 ||
         (kl != KNN_I8_KL_S && kl != KNN_I8_KL))
         return KNN_ERR_INVALID;
@@ -2292,7 +2355,7 @@ extern "C" int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const dou
 #define RANK(T, KP, KL)                                                                            \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge_rank<T, KP, KL>), grid, dim3(256), lds, s, part_d, part_i, \
                        part_T, nsplit, lpq, nq, nq_pad, first_step, st_d, st_x, st_i, st_T, k,       \
-                       (unsigned long long *)qthr, cap)
+                       (unsigned long long *)qthr, cap, fin, fa)
     if (dtype == KNN_F64 && kp == KNN_KP && kl == KNN_I8_KL_S) RANK(double, KNN_KP, KNN_I8_KL_S);
     else if (dtype == KNN_F64 && kp == KNN_KP) RANK(double, KNN_KP, KNN_I8_KL);
     else if (dtype == KNN_F32 && kp == KNN_KP && kl == KNN_I8_KL_S) RANK(float, KNN_KP, KNN_I8_KL_S);
