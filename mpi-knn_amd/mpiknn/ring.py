@@ -71,6 +71,8 @@ class GpuEngine:
         import os
         self.try_s8 = n <= 896 and os.environ.get("KNN_NO_S8", "0") != "1"
         self.spec = False
+        self.spec_hint = None      # the host meta of the last search begun from the byte block
+        self._meta_pinned = None
         self._src = None
         self.sq = None
 
@@ -117,6 +119,14 @@ class GpuEngine:
             return src.stride(1), self.mk.COLMAJOR, ("f32" if src.dtype == self.torch.float32 else "f64")
         assert src.stride(1) == 1
         return src.stride(0), self.mk.ROWMAJOR, ("f32" if src.dtype == self.torch.float32 else "f64")
+
+    def meta_host(self, meta):
+        """an asynchronous read-back of meta into pinned host memory (valid
+        once the current stream has passed this point)"""
+        if self._meta_pinned is None:
+            self._meta_pinned = self.torch.empty(self.mk.META_DOUBLES, dtype=self.torch.float64, pin_memory=True)
+        self._meta_pinned.copy_(meta, non_blocking=True)
+        return self._meta_pinned
 
     def pack_elements(self):
         """the element block of the last pack's source into qb (the exact
@@ -235,8 +245,19 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
         dist.all_reduce(engine.meta, op=dist.ReduceOp.MAX)
         h_meta = engine.meta.cpu().numpy()   # the ring needs it on the host anyway
     spec = getattr(engine, "spec", False)
+    verify = None
     if h_meta is None and spec:
-        h_meta = engine.meta.cpu().numpy()   # (P = 1: begin would read it back anyway)
+        hint = getattr(engine, "spec_hint", None)
+        if hint is not None:
+            # P = 1 and the last search's meta accepted the byte block: start
+            # without waiting for this one's read-back (the host would sit in
+            # a stream sync while the GPU idles); the meta is read back
+            # behind the search and checked after it -- on a mismatch the
+            # search runs again from the element block
+            h_meta = hint
+            verify = engine.meta_host(engine.meta)
+        else:
+            h_meta = engine.meta.cpu().numpy()   # (P = 1: begin would read it back anyway)
     if h_meta is not None and h_meta[7] != 0.0 and not engine.mk.s8_spec_ok(h_meta, engine.n, engine.dtype):
         # some rank packed the speculative byte block (meta word 7) and the
         # reduced meta rejects it: every rank packs its element block and
@@ -254,6 +275,8 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
         wire = (os.environ.get("KNN_NO_WIRE", "0") != "1" and hasattr(engine, "wires") and
                 engine.mk.wire_ok(h_meta))
     engine.begin(q_base, h_meta=h_meta)
+    if spec and P == 1 and verify is None:
+        engine.spec_hint = h_meta
     # byte / fp16 shadow blocks are what the steps fold (and the ring moves);
     # at P = 1 only a search begun from the byte block folds it explicitly
     shadow = ((P > 1 or spec) and hasattr(engine, "step_shadow") and engine.ctx.shadow() != 0 and
@@ -376,6 +399,12 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
     else:
         one_pass(0, False)
     unresolved = engine.end()
+    if verify is not None:
+        # (the read-back was enqueued before the search's first kernel, which
+        # the merge end() synchronised with waits for: it has landed)
+        if not engine.mk.s8_spec_ok(verify.numpy(), engine.n, engine.dtype):
+            engine.spec_hint = None   # not this data: the checked path, from the start
+            return ring_search(dist, torch, engine, rank, P, m, q_base, schedule)
     total = unresolved
     if P > 1:
         t = torch.tensor([float(unresolved)], dtype=torch.float64, device=engine.meta.device)

@@ -175,3 +175,26 @@ def test_s8_fallback(knn, oracle, P, kind):
         ref = oracle.knn(X, 30, rows=(base, rows))
         assert np.array_equal(got["idx"], ref["idx"]), (kind, P, g)
         assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), (kind, P, g)
+
+
+def test_s8_speculative_begin_and_mismatch(knn, oracle):
+    """P = 1: after a search begun from the byte block, the next one starts
+    without reading its meta back (the last one's host meta as the hint) and
+    checks it after the search; data the byte block cannot hold (a negative
+    value) is then searched again from the element block -- every result
+    equal to the oracle's."""
+    import torch
+    import mpiknn.ring as ring
+    X = datasets.mnist_like(1500, 196, seed=8)[0]
+    m, n = X.shape
+    e = ring.GpuEngine(torch, 0, n, m, m, 30)
+    for trial, Y in enumerate((X, X[::-1].copy(), np.where(X > 100, X - 200.0, X))):
+        e.try_s8 = True
+        e.pack(torch.from_numpy(np.ascontiguousarray(Y)).to("cuda:0"), layout_col=False)
+        assert e.spec
+        ring.ring_search(None, torch, e, 0, 1, m, 0)
+        got = e.result()
+        ref = oracle.knn(Y, 30)
+        assert np.array_equal(got["idx"], ref["idx"]), trial
+        assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), trial
+        assert (e.spec_hint is not None) == (trial < 2), trial
