@@ -504,8 +504,9 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     };
     // The shared bound may fall while the workgroup runs (other splits end,
     // and the merge of an earlier ring step publishes the running answer
-    // while a fused launch runs), so W = 8 workgroups re-read it about once
-    // a tile.  The load is issued from asm, invisible to the compiler's wait
+    // while a fused launch runs), so W = 8 workgroups re-read it every
+    // second tile of several chunks (every tile: 1.3% slower at P = 1, no
+    // better at P = 8), every tile when a tile is one chunk (sift).  The load is issued from asm, invisible to the compiler's wait
     // pass: a plain load made it drain every LDS-DMA piece in flight
     // (vmcnt(0)) before the value's first use.  It is complete once the ring
     // has waited past the pieces staged after it (wait_next: all but the
@@ -574,7 +575,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         if constexpr (W == 8) {
             if (qthr != nullptr) {
                 if (q_ready >= 0 && xdone > q_ready) qthr_apply();
-                if (q_ready < 0) qthr_issue(s_x);
+                if (q_ready < 0 && (NCH == 1 || (t & 1) == 0)) qthr_issue(s_x);   // mnist: 3.89 -> 3.84 ms (kbench8)
             }
         }
         int T = thr_v();
