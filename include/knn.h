@@ -34,6 +34,8 @@
  *   KNN_NO_RANK_MERGE=1   int8 lists merged by k_merge's argmin rounds
  *                         instead of k_merge_rank
  *   KNN_FORCE_RESCAN=1    send every query through the exact rescan pass
+ *   KNN_NO_RESEARCH8=1    no int8 re-search (65-entry lists) of uncertified
+ *                         queries of a single-block search before the rescan
  *   KNN_FORCE_RING=1      knn_search runs the ring driver on one GPU
  *   KNN_RING_SCHEDULE=ring|direct
  *                         ring driver schedule: "ring" = the reference's

@@ -105,6 +105,20 @@ struct knn_ctx {
     int split_next;
     int nfail;
     int mode;
+    /* the int8 re-search of uncertified queries (knn_ctx_end, single-block
+     * searches): host meta of the search, the step's block, a sub-context
+     * with 65-entry lane lists and its buffers */
+    double hmeta[KNN_META_DOUBLES];
+    int have_hmeta;
+    int force_long;           /* this context is such a sub-context */
+    int one_block_q8;         /* the search's only step folded its own query byte block */
+    size_t step0_nc, step0_cbase;
+    struct knn_ctx *sub;
+    size_t sub_cap;
+    void *sub_q8;
+    knn_neighbour_t *sub_out;
+    unsigned char *sub_flag;
+    int *fail_list2;
     /* kernel timing (knn_ctx_profile): 3 events per step bracket
      * k_dist_topk and k_merge */
     int prof_on, prof_pending, prof_launches;
@@ -252,6 +266,11 @@ int knn_block_pack(void *d_block, size_t cap, size_t rows, size_t n, const doubl
 
 static void ctx_free_buffers(knn_ctx_t *c)
 {
+    if (c->sub) knn_ctx_destroy(c->sub);
+    hipFree(c->sub_q8);
+    hipFree(c->sub_out);
+    hipFree(c->sub_flag);
+    hipFree(c->fail_list2);
     for (int b = 0; b < KNN_PSETS; b++) {
         if (c->ev_m[b]) hipEventDestroy(c->ev_m[b]);
         if (c->ev_ds[b]) hipEventDestroy(c->ev_ds[b]);
@@ -560,6 +579,8 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
     const int no_i8 = env_on("KNN_NO_I8"), no_h16 = env_on("KNN_NO_H16"), no_split = env_on("KNN_NO_SPLIT");
     c->split = 0;
     c->sscale = 0.f;
+    c->have_hmeta = 0;
+    c->one_block_q8 = 0;
     if (!(no_i8 && no_h16 && no_split)) {
         double hm[KNN_META_DOUBLES];
         if (!h_meta) {
@@ -567,6 +588,8 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
             HIPCHK(hipStreamSynchronize((hipStream_t)stream));
             h_meta = hm;
         }
+        memcpy(c->hmeta, h_meta, sizeof(c->hmeta));
+        c->have_hmeta = 1;
         c->i8 = !no_i8 && knn_i8_exact(h_meta, c->n, c->dtype);
         if (d_s8 && !c->i8) return KNN_ERR_INVALID;
         c->h16 = !c->i8 && !no_h16 && knn_h16_exact(h_meta, c->n, c->dtype);
@@ -575,10 +598,11 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
             c->split = c->sscale > 0.f;
         }
     }
-    c->lpq = c->i8 ? knn_i8_lpq(c->kp) : 4;
-    /* int8 lane lists: 12 entries (k <= 32), 17 on request (KNN_I8_KL=17) */
-    c->klx = c->i8 ? knn_i8_kl(c->kp) : c->kl;
-    if (c->i8 && c->klx == KNN_I8_KL_S && getenv("KNN_I8_KL") && atoi(getenv("KNN_I8_KL")) == KNN_I8_KL)
+    c->lpq = c->i8 ? (c->force_long ? 2 : knn_i8_lpq(c->kp)) : 4;
+    /* int8 lane lists: 12 entries (k <= 32), 17 on request (KNN_I8_KL=17),
+     * 65 in the re-search sub-context */
+    c->klx = c->i8 ? (c->force_long ? KNN_I8_KL_L : knn_i8_kl(c->kp)) : c->kl;
+    if (c->i8 && !c->force_long && c->klx == KNN_I8_KL_S && getenv("KNN_I8_KL") && atoi(getenv("KNN_I8_KL")) == KNN_I8_KL)
         c->klx = KNN_I8_KL;
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
      * element fragments in the kernel instead) */
@@ -1058,6 +1082,9 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
         HIPCHK(hipEventRecord(ev[0], ds));
     }
     if (c->i8) {
+        c->one_block_q8 = c->nstep == 0 && !xb && csh == c->q8;
+        c->step0_nc = nc;
+        c->step0_cbase = c_base;
         if (!xb) {
             tab.nblk = 1;
             tab.ptr[0] = csh;
@@ -1164,6 +1191,62 @@ int knn_ctx_step_shadow_n(knn_ctx_t *c, int nblk, const void *const *d_sblocks, 
 
 int knn_ctx_shadow(const knn_ctx_t *c) { return c ? c->shadow : 0; }
 
+/* Uncertified queries of a single-block int8 search (P = 1: the block is
+ * the query block, resident as q8) are searched again on the int8
+ * contraction with 65-entry lane lists -- a lane can then only overflow if
+ * more than 64 rows tie at or below the query's (k+1)-th distance -- and
+ * the certified results replace the fp64 rescan for them; what stays
+ * uncertified (ties beyond that) goes to the exact rescan as before.  SIFT
+ * (1M x 128, k = 32): 186 queries, 8.4 ms of fp64 scan. */
+static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
+{
+    if (!c->i8 || c->force_long || !c->one_block_q8 || c->nstep != 1 || !c->have_hmeta ||
+        c->step0_cbase != c->q_base || c->q_rows_pad != knn_rows_pad(c->block_cap) || c->kp > KNN_KP_M ||
+        env_on("KNN_FORCE_RESCAN") || env_on("KNN_NO_RESEARCH8"))
+        return KNN_OK;
+    const int nf = c->nfail;
+    if (!c->sub || c->sub_cap < (size_t)nf) {
+        if (c->sub) knn_ctx_destroy(c->sub);
+        c->sub = NULL;
+        hipFree(c->sub_q8);
+        hipFree(c->sub_out);
+        hipFree(c->sub_flag);
+        c->sub_q8 = NULL;
+        c->sub_out = NULL;
+        c->sub_flag = NULL;
+        const size_t cap = knn_round_up((size_t)nf, KNN_TQ);
+        RCHK(knn_ctx_create_dt(&c->sub, c->device, cap, c->n, c->block_cap, c->k, c->dtype));
+        c->sub->force_long = 1;
+        c->sub_cap = cap;
+        if (hipMalloc(&c->sub_q8, knn_s8_bytes(cap, c->n)) != hipSuccess ||
+            hipMalloc((void **)&c->sub_out, cap * (size_t)c->k * sizeof(knn_neighbour_t)) != hipSuccess ||
+            hipMalloc((void **)&c->sub_flag, cap) != hipSuccess)
+            return KNN_ERR_NOMEM;
+        if (!c->fail_list2 && hipMalloc((void **)&c->fail_list2, c->nq_pad * sizeof(int)) != hipSuccess)
+            return KNN_ERR_NOMEM;
+    }
+    knn_ctx_t *u = c->sub;
+    u->nq = (size_t)nf;   /* within the capacity it was created with */
+    u->nq_pad = knn_round_up((size_t)nf, KNN_TQ);
+    RCHK(knn_launch_gather8(c->sub_q8, c->q8, c->fail_list, nf, c->n, c->q_rows_pad, knn_rows_pad(c->sub_cap), s));
+    /* q_base past every row id: no row is masked as "the query itself"
+     * (its d^2 = 0 is dropped like every exact duplicate, serial:86) */
+    RCHK(ctx_begin(u, NULL, c->sub_q8, c->sub_cap, (size_t)1 << 30, c->meta, c->hmeta, s));
+    RCHK(ctx_step_impl(u, NULL, c->q8, c->step0_nc, c->step0_cbase, NULL, s));
+    size_t un2 = 0;
+    RCHK(knn_ctx_end(u, c->sub_out, &un2, s));
+    RCHK(knn_launch_resolve8(c->sub_flag, c->fail_list, nf, u->fail_list, u->fail_count, c->sub_out, c->k, d_out,
+                             c->fail_list2, c->fail_count, s));
+    int nn = 0;
+    HIPCHK(hipMemcpyAsync(&nn, c->fail_count, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int *t = c->fail_list;
+    c->fail_list = c->fail_list2;
+    c->fail_list2 = t;
+    c->nfail = nn;
+    return KNN_OK;
+}
+
 int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *stream)
 {
     if (!c || !d_out || c->first_step) return KNN_ERR_INVALID;
@@ -1193,6 +1276,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     RCHK(prof_collect(c));
     c->nfail = host[0];
     c->mode = host[1];
+    if (c->nfail > 0) RCHK(research8(c, d_out, s));
     if (unresolved) *unresolved = (size_t)c->nfail;
     if (c->nfail > 0) {
         const size_t need = (size_t)c->nfail * (1 + (size_t)knn_rescan_chunks(c->nfail));

@@ -722,6 +722,77 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
 }
 
 // ---------------------------------------------------------------------------
+// Re-search of uncertified queries on the int8 contraction (knn_ctx_end,
+// single-block searches): their byte rows gathered into a query block of
+// their own, searched again with 65-entry lane lists, and the certified
+// results scattered back.
+// ---------------------------------------------------------------------------
+// dst row i = src row list[i] (bytes and norm word; rows >= cnt zero)
+__global__ __launch_bounds__(256) void k_gather8(signed char *__restrict__ dst, const signed char *__restrict__ src,
+                                                 const int *__restrict__ list, int cnt, int rs, size_t src_rows_pad,
+                                                 size_t dst_rows_pad)
+{
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int *sn = (const int *)(src + src_rows_pad * (size_t)rs);
+    int *dn = (int *)(dst + dst_rows_pad * (size_t)rs);
+    for (size_t r = (size_t)blockIdx.x * 4 + wave; r < dst_rows_pad; r += (size_t)gridDim.x * 4) {
+        const int q = r < (size_t)cnt ? list[r] : -1;
+        for (int b = 4 * lane; b < rs; b += 256)
+            *(int *)(dst + r * rs + b) = q >= 0 ? *(const int *)(src + (size_t)q * rs + b) : 0;
+        if (lane == 0) {
+            const int nrm = q >= 0 ? -(sn[i8_norm_pos(q)] >> 5) : 0;
+            dn[i8_norm_pos((int)r)] = i8_norm_word((int)r, nrm);
+        }
+    }
+}
+
+// flag[i] = 1 for the re-searched queries still uncertified (flag zeroed first)
+__global__ void k_flag8_set(unsigned char *__restrict__ flag, const int *__restrict__ sub_fail,
+                            const int *__restrict__ sub_cnt)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < *sub_cnt) flag[sub_fail[j]] = 1;
+}
+// certified re-searched queries: records into out; the rest onto a new list
+__global__ void k_resolve8(const unsigned char *__restrict__ flag, const int *__restrict__ list, int cnt,
+                           const knn_neighbour_t *__restrict__ sub_out, int k, knn_neighbour_t *__restrict__ out,
+                           int *__restrict__ new_list, int *__restrict__ new_cnt)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = t / k, r = t - i * k;
+    if (i >= cnt) return;
+    if (flag[i]) {
+        if (r == 0) new_list[atomicAdd(new_cnt, 1)] = list[i];
+        return;
+    }
+    out[(size_t)list[i] * k + r] = sub_out[(size_t)i * k + r];
+}
+
+extern "C" int knn_launch_gather8(void *dst, const void *src, const int *list, int cnt, size_t n,
+                                  size_t src_rows_pad, size_t dst_rows_pad, void *stream)
+{
+    const int rs = (int)knn_s8_rs(n);
+    const unsigned grid = (unsigned)((dst_rows_pad + 3) / 4 < 1024 ? (dst_rows_pad + 3) / 4 : 1024);
+    hipLaunchKernelGGL(k_gather8, dim3(grid), dim3(256), 0, (hipStream_t)stream, (signed char *)dst,
+                       (const signed char *)src, list, cnt, rs, src_rows_pad, dst_rows_pad);
+    return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
+}
+
+extern "C" int knn_launch_resolve8(unsigned char *flag, const int *list, int cnt, const int *sub_fail,
+                                   const int *sub_cnt, const knn_neighbour_t *sub_out, int k,
+                                   knn_neighbour_t *out, int *new_list, int *new_cnt, void *stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    if (cnt <= 0) return KNN_OK;
+    if (hipMemsetAsync(flag, 0, (size_t)cnt, s) != hipSuccess || hipMemsetAsync(new_cnt, 0, sizeof(int), s) != hipSuccess)
+        return KNN_ERR_HIP;
+    hipLaunchKernelGGL(k_flag8_set, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, flag, sub_fail, sub_cnt);
+    hipLaunchKernelGGL(k_resolve8, dim3((unsigned)(((size_t)cnt * k + 255) / 256)), dim3(256), 0, s, flag, list,
+                       cnt, sub_out, k, out, new_list, new_cnt);
+    return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 extern "C" int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,

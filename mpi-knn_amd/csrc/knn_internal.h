@@ -124,6 +124,12 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
 /* fp16 shadow rows (round_up(n, 64) halves a row) of a packed block */
 int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);
+/* int8 re-search of uncertified queries (knn_i8.hip) */
+int knn_launch_gather8(void *dst, const void *src, const int *list, int cnt, size_t n, size_t src_rows_pad,
+                       size_t dst_rows_pad, void *stream);
+int knn_launch_resolve8(unsigned char *flag, const int *list, int cnt, const int *sub_fail, const int *sub_cnt,
+                        const knn_neighbour_t *sub_out, int k, knn_neighbour_t *out, int *new_list, int *new_cnt,
+                        void *stream);
 /* speculative byte block straight from the source (knn_block_pack_s8) */
 int knn_launch_pack_s8(void *dst, int dtype, size_t cap, size_t rows, size_t n, const void *src, int src_dtype,
                        size_t ld, int layout, void *stream);

@@ -198,3 +198,33 @@ def test_s8_speculative_begin_and_mismatch(knn, oracle):
         assert np.array_equal(got["idx"], ref["idx"]), trial
         assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), trial
         assert (e.spec_hint is not None) == (trial < 2), trial
+
+
+def test_int8_research_of_uncertified(knn, oracle, monkeypatch):
+    """Queries a 12-entry lane list cannot certify (tight clusters: most of a
+    query's k + 1 nearest fall in one lane) are searched again on the int8
+    contraction with 65-entry lists before any fp64 rescan; the results stay
+    the oracle's, and fewer (here: no) queries reach the exact rescan."""
+    import torch
+    import mpiknn.ring as ring
+    rng = np.random.default_rng(21)
+    base = rng.integers(20, 236, (120, 64)).astype(np.float64)
+    X = np.repeat(base, 25, axis=0) + rng.integers(-2, 3, (3000, 64))
+    m, n = X.shape
+    counts = {}
+    for mode in ("off", "on"):
+        if mode == "off":
+            monkeypatch.setenv("KNN_NO_RESEARCH8", "1")
+        else:
+            monkeypatch.delenv("KNN_NO_RESEARCH8", raising=False)
+        e = ring.GpuEngine(torch, 0, n, m, m, 30)
+        e.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
+        counts[mode] = ring.ring_search(None, torch, e, 0, 1, m, 0)
+        assert e.ctx.contraction_bits() == 8
+        got = e.result()
+        ref = oracle.knn(X, 30)
+        assert np.array_equal(got["idx"], ref["idx"]), mode
+        assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), mode
+    if counts["off"] == 0:
+        pytest.skip("no uncertified queries on this data")
+    assert counts["on"] < counts["off"], counts
