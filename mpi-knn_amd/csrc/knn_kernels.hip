@@ -378,11 +378,14 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
 }
 
 // row-major source: one wave per row, lane l converts the 8-element groups
-// l, l + 64, ... (one 8-byte store each)
-template <typename T, typename S>
+// l, l + 64, ... (one 8-byte store each); VEC: 16-byte-aligned rows, whole
+// groups read as 16-byte vectors (sift: 0.68 ms for 512 MB with scalar loads)
+template <typename T, typename S, bool VEC>
 __global__ __launch_bounds__(256) void k_pack8_row(signed char *__restrict__ dst, size_t rows, size_t rows_pad,
                                                    int n, int rs, const S *__restrict__ src, size_t ld)
 {
+    typedef typename std::conditional<sizeof(S) == 8, dbl2, flt4>::type svec_t;
+    constexpr int SV = 16 / (int)sizeof(S);
     int *norms = (int *)(dst + rows_pad * (size_t)rs);
     double *meta = (double *)(norms + rows_pad);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -395,11 +398,23 @@ __global__ __launch_bounds__(256) void k_pack8_row(signed char *__restrict__ dst
         const S *x = src + r * ld;
         for (int g = lane; g < ng; g += 64) {
             unsigned lo = 0u, hi = 0u;
+            S sv[8];
+            if (VEC && r < rows && 8 * g + 8 <= n) {
+#pragma unroll
+                for (int q = 0; q < 8 / SV; q++) {
+                    const svec_t w = *(const svec_t *)(x + 8 * g + SV * q);
+#pragma unroll
+                    for (int e = 0; e < SV; e++) sv[SV * q + e] = w[e];
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++) sv[e] = (r < rows && 8 * g + e < n) ? x[8 * g + e] : (S)0;
+            }
 #pragma unroll
             for (int e = 0; e < 8; e++) {
                 const int j = 8 * g + e;
                 const bool in = r < rows && j < n;
-                const T v = in ? (T)x[j] : (T)0;
+                const T v = in ? (T)sv[e] : (T)0;
                 ma.add((double)v, s);
                 const int xi = in ? knn_spec8(v) : 0;
                 si += (unsigned)(xi * xi);
@@ -2011,8 +2026,13 @@ static int launch_pack8(signed char *dst, size_t cap, size_t rows, size_t n, con
                            dst, rows, rp, (int)n, (int)rs, src, ld);
     } else {
         const unsigned nb = (unsigned)((rp + 3) / 4 < 8192 ? (rp + 3) / 4 : 8192);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_row<T, S>), dim3(nb), dim3(256), 0, s, dst, rows, rp, (int)n,
-                           (int)rs, src, ld);
+        const bool vec = ((uintptr_t)src % 16 == 0) && (ld * sizeof(S)) % 16 == 0;
+        if (vec)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_row<T, S, true>), dim3(nb), dim3(256), 0, s, dst, rows, rp,
+                               (int)n, (int)rs, src, ld);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_row<T, S, false>), dim3(nb), dim3(256), 0, s, dst, rows, rp,
+                               (int)n, (int)rs, src, ld);
     }
     return hip_status();
 }
