@@ -100,8 +100,13 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        from mpiknn.ring import ring_timeout_s
+        # a stalled or dead peer ends the run (RCCL watchdog) instead of
+        # hanging it: the bound of every ring exchange (mpiknn/ring.py)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(seconds=ring_timeout_s()))
     P = world
 
     res = run_workload(args.workload, args.steps, args.warmup, args, torch, dist, rank, P, local,

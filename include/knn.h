@@ -45,6 +45,12 @@
  *                         gloo -- no multi-GPU node has run it yet)
  *   KNN_RING_FUSE=rest|all direct schedule: own block folded beside the
  *                         exchange (rest) or with the received blocks (all)
+ *   KNN_RING_TIMEOUT_S=t  bound (seconds, default 300) on every wait for the
+ *                         ring's transfers: RCCL asynchronous errors are
+ *                         polled beside it, and a failed or stalled transfer
+ *                         aborts the communicators and returns KNN_ERR_RCCL
+ *                         (mpiknn/ring.py: RingError; bench.py: the process
+ *                         group's timeout)
  *   KNN_RING_LOOPBACK=1   P virtual ranks on device 0 (tests)
  *   KNN_NO_SHADOW_RING=1  ring moves element blocks, not shadow/byte blocks
  *   KNN_MAT / KNN_MPI_COMPAT  the CLIs: .mat path, bug-compatible mode
@@ -329,8 +335,11 @@ KNN_API int knn_ctx_step_shadow_n(knn_ctx_t *ctx, int nblk, const void *const *d
  * could not be certified exact; if > 0 the caller runs one more pass over
  * every block with knn_ctx_rescan_step() then knn_ctx_rescan_end().  The
  * records are written behind the last merge on the context's own stream,
- * not after work pending on `stream`: d_out must not be in use by pending
- * work; `stream` is ordered after the records on return. */
+ * which first waits for `stream` as it stands at the call (so d_out may have
+ * just been allocated, cleared or read on `stream`); `stream` is ordered
+ * after the records on return.  A search begun with knn_ctx_begin_s8 whose
+ * device meta turns out not to be INT-exact reports every query unresolved
+ * (nothing is read through the missing element block). */
 KNN_API int knn_ctx_end(knn_ctx_t *ctx, knn_neighbour_t *d_out, size_t *unresolved,
                 void *stream);
 KNN_API int knn_ctx_rescan_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,

@@ -1198,40 +1198,52 @@ int knn_ctx_shadow(const knn_ctx_t *c) { return c ? c->shadow : 0; }
  * the certified results replace the fp64 rescan for them; what stays
  * uncertified (ties beyond that) goes to the exact rescan as before.  SIFT
  * (1M x 128, k = 32): 186 queries, 8.4 ms of fp64 scan. */
+static void research8_free(knn_ctx_t *c)
+{
+    if (c->sub) knn_ctx_destroy(c->sub);
+    hipFree(c->sub_q8);
+    hipFree(c->sub_out);
+    hipFree(c->sub_flag);
+    c->sub = NULL;
+    c->sub_q8 = NULL;
+    c->sub_out = NULL;
+    c->sub_flag = NULL;
+    c->sub_cap = 0;
+}
+
 static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
 {
-    if (!c->i8 || c->force_long || !c->one_block_q8 || c->nstep != 1 || !c->have_hmeta ||
+    /* INT mode only (c->mode: the device's verdict on the real meta): a
+     * speculative begin (knn_ctx_begin_s8 on a stale host hint) whose data
+     * turned out real-valued fails every query in GEMM mode, and the
+     * sub-search would run GEMM work from a context with no element rows */
+    if (c->mode != KNN_MODE_INT || !c->i8 || c->force_long || !c->one_block_q8 || c->nstep != 1 || !c->have_hmeta ||
         c->step0_cbase != c->q_base || c->q_rows_pad != knn_rows_pad(c->block_cap) || c->kp > KNN_KP_M ||
         env_on("KNN_FORCE_RESCAN") || env_on("KNN_NO_RESEARCH8"))
         return KNN_OK;
     const int nf = c->nfail;
     if (!c->sub || c->sub_cap < (size_t)nf) {
-        if (c->sub) knn_ctx_destroy(c->sub);
-        c->sub = NULL;
-        hipFree(c->sub_q8);
-        hipFree(c->sub_out);
-        hipFree(c->sub_flag);
-        c->sub_q8 = NULL;
-        c->sub_out = NULL;
-        c->sub_flag = NULL;
+        research8_free(c);
         const size_t cap = knn_round_up((size_t)nf, KNN_TQ);
         RCHK(knn_ctx_create_dt(&c->sub, c->device, cap, c->n, c->block_cap, c->k, c->dtype));
         c->sub->force_long = 1;
-        c->sub_cap = cap;
         if (hipMalloc(&c->sub_q8, knn_s8_bytes(cap, c->n)) != hipSuccess ||
             hipMalloc((void **)&c->sub_out, cap * (size_t)c->k * sizeof(knn_neighbour_t)) != hipSuccess ||
-            hipMalloc((void **)&c->sub_flag, cap) != hipSuccess)
+            hipMalloc((void **)&c->sub_flag, cap) != hipSuccess ||
+            (!c->fail_list2 && hipMalloc((void **)&c->fail_list2, c->nq_pad * sizeof(int)) != hipSuccess)) {
+            research8_free(c);   /* no half-built sub-context survives */
             return KNN_ERR_NOMEM;
-        if (!c->fail_list2 && hipMalloc((void **)&c->fail_list2, c->nq_pad * sizeof(int)) != hipSuccess)
-            return KNN_ERR_NOMEM;
+        }
+        c->sub_cap = cap;   /* only once every buffer exists */
     }
     knn_ctx_t *u = c->sub;
     u->nq = (size_t)nf;   /* within the capacity it was created with */
     u->nq_pad = knn_round_up((size_t)nf, KNN_TQ);
     RCHK(knn_launch_gather8(c->sub_q8, c->q8, c->fail_list, nf, c->n, c->q_rows_pad, knn_rows_pad(c->sub_cap), s));
-    /* q_base past every row id: no row is masked as "the query itself"
-     * (its d^2 = 0 is dropped like every exact duplicate, serial:86) */
-    RCHK(ctx_begin(u, NULL, c->sub_q8, c->sub_cap, (size_t)1 << 30, c->meta, c->hmeta, s));
+    /* q_base just past the block's last row id: no row is masked as "the
+     * query itself" (its d^2 = 0 is dropped like every exact duplicate,
+     * serial:86) */
+    RCHK(ctx_begin(u, NULL, c->sub_q8, c->sub_cap, c->step0_cbase + c->step0_nc, c->meta, c->hmeta, s));
     RCHK(ctx_step_impl(u, NULL, c->q8, c->step0_nc, c->step0_cbase, NULL, s));
     size_t un2 = 0;
     RCHK(knn_ctx_end(u, c->sub_out, &un2, s));
@@ -1256,8 +1268,13 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
      * behind the last merge: every cross-stream wait (hipStreamWaitEvent)
      * put ~20 us of latency on the pass's critical path, even when the
      * event had long completed (rocprofv3 of the P = 8 ring emulation).
-     * d_out must not be in use by work pending on other streams (knn.h);
-     * the caller's stream is ordered after the results. */
+     * The records go to d_out from the merge stream, so that stream first
+     * waits for the caller's stream as it stands now: d_out may have just
+     * been allocated, cleared or read there (a caching allocator hands out
+     * memory that pending work on the caller's stream used last).  The
+     * caller's stream is ordered after the results. */
+    HIPCHK(hipEventRecord(c->ev_in, s));
+    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_in, 0));
     /* the last merge (deferred or pending) finalizes too when it is the
      * rank merge (INT-mode int8 lists) */
     int fin = 0;
@@ -1276,7 +1293,13 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     RCHK(prof_collect(c));
     c->nfail = host[0];
     c->mode = host[1];
-    if (c->nfail > 0) RCHK(research8(c, d_out, s));
+    if (c->nfail > 0 && research8(c, d_out, s) != KNN_OK) {
+        /* the re-search is an optimisation: on any failure of it the exact
+         * rescan resolves the same queries (the fail list is untouched until
+         * research8's last step, which cannot fail) */
+        HIPCHK(hipStreamSynchronize(s));
+        (void)hipGetLastError();
+    }
     if (unresolved) *unresolved = (size_t)c->nfail;
     if (c->nfail > 0) {
         const size_t need = (size_t)c->nfail * (1 + (size_t)knn_rescan_chunks(c->nfail));

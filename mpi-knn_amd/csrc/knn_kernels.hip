@@ -1310,8 +1310,14 @@ __global__ __launch_bounds__(256) void k_merge(
     // 2E has S > d^2_k + E >= the k-th smallest nonzero S of the state, now
     // and after any later merge (d^2_k only falls), so it can never reach
     // the top k: its S is skipped and marked +inf (k_finalize ignores it).
+    // A context begun from a byte block alone (knn_ctx_begin_s8) holds no
+    // element rows: if the device meta says GEMM after all (a speculative
+    // begin on data that did not qualify), no exact S is computed -- the new
+    // entries get S = +inf and k_finalize fails every query (it sees no
+    // query norms either) instead of reading through a null block
+    const bool exact_ok = mode == KNN_MODE_GEMM && qblk != nullptr;
     double win = KNN_INF;
-    if (mode == KNN_MODE_GEMM) {
+    if (exact_ok) {
         const double E = qv ? knn_cert_E<TE>(n, (double)qblk[qnorm_off + q], meta[KNN_META_MAXNORM], filt,
                                              meta[KNN_META_MAXABS])
                             : 0.0;
@@ -1336,7 +1342,7 @@ __global__ __launch_bounds__(256) void k_merge(
         if (qv && sl + S * x < KP && mode == KNN_MODE_GEMM && si[x] >= 0) {
             if (ssrc[x]) {
                 sx[x] = st_x[(size_t)q * KP + spos[x]];
-            } else if (sd[x] <= win) {
+            } else if (exact_ok && sd[x] <= win) {
                 const int row = (int)((long)si[x] - (long)c_base);
                 sx[x] = knn_exact_sq_v<TE>(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n);
             } else {
@@ -1568,7 +1574,10 @@ __global__ __launch_bounds__(256) void k_finalize(
     if (q >= nq) return;
     knn_neighbour_t *o = out + (size_t)q * k;
 
-    if (mode == KNN_MODE_SCAN || force_fail) {   // force_fail: tests of the rescan pass
+    // force_fail: tests of the rescan pass; no query norms (a context begun
+    // from a byte block alone, knn_ctx_begin_s8) outside INT mode: nothing
+    // exact to certify with -- every query takes the rescan
+    if (mode == KNN_MODE_SCAN || force_fail || (mode != KNN_MODE_INT && qnorm == nullptr)) {
         if (lane == 0) {
             fail_list[atomicAdd(fail_count, 1)] = q;
             fbound[q] = KNN_INF;

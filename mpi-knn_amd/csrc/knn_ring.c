@@ -120,6 +120,59 @@ static int ring_hop(ring_dev_t *d, int P, size_t bytes, ring_transport_t *t)
     return KNN_OK;
 }
 
+/* Bounded wait (KNN_RING_TIMEOUT_S, default 300 s) for one stream of every
+ * device: `comm` = the comm streams (every transfer of a pass), else the
+ * compute streams (the meta all-reduce runs there).  RCCL: polls each
+ * communicator's asynchronous error beside the streams, and on an error or
+ * the deadline aborts every communicator (the caller then skips
+ * ncclCommDestroy) and returns KNN_ERR_RCCL -- a dead peer or a transfer that
+ * never completes ends the search with a status instead of a hang in a
+ * later stream synchronisation.  Loopback: the fabric stream. */
+static double ring_timeout_s(void)
+{
+    const char *e = getenv("KNN_RING_TIMEOUT_S");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0.0 ? v : 300.0;
+}
+
+static int ring_drain(ring_dev_t *d, int P, ring_transport_t *t, int comm, int *aborted)
+{
+    const double deadline = now_s() + ring_timeout_s();
+    for (;;) {
+        int pending = 0, bad = 0;
+        if (t->kind == RING_LOOPBACK && comm) {
+            if (hipSetDevice(d[0].dev) != hipSuccess) return KNN_ERR_HIP;
+            const hipError_t q = hipStreamQuery(t->fabric);
+            if (q == hipErrorNotReady) pending = 1;
+            else if (q != hipSuccess) return KNN_ERR_HIP;
+        } else {
+            for (int g = 0; g < P; g++) {
+                if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
+                const hipError_t q = hipStreamQuery(comm ? d[g].ms : d[g].cs);
+                if (q == hipErrorNotReady) pending = 1;
+                else if (q != hipSuccess) return KNN_ERR_HIP;
+                if (t->kind == RING_RCCL && d[g].comm) {
+                    ncclResult_t st = ncclSuccess;
+                    if (ncclCommGetAsyncError(d[g].comm, &st) != ncclSuccess ||
+                        (st != ncclSuccess && st != ncclInProgress))
+                        bad = 1;
+                }
+            }
+        }
+        if (!pending && !bad) return KNN_OK;
+        if (bad || now_s() > deadline) {
+            if (t->kind == RING_RCCL) {
+                for (int g = 0; g < P; g++)
+                    if (d[g].comm) ncclCommAbort(d[g].comm);
+                *aborted = 1;
+            }
+            return t->kind == RING_RCCL ? KNN_ERR_RCCL : KNN_ERR_HIP;
+        }
+        const struct timespec ts = {0, 50000};   /* 50 us */
+        nanosleep(&ts, NULL);
+    }
+}
+
 static size_t rows_of(int b, size_t R, size_t m)
 {
     const size_t base = (size_t)b * R;
@@ -332,7 +385,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
     int devs[KNN_RING_MAX];
     ncclComm_t comms[KNN_RING_MAX];
     memset(comms, 0, sizeof(comms));
-    int rc = KNN_OK;
+    int rc = KNN_OK, aborted = 0;
     for (int g = 0; g < P; g++) devs[g] = tr.kind == RING_LOOPBACK ? 0 : g;
     if (tr.kind == RING_RCCL) {
         if (ncclCommInitAll(comms, P, devs) != ncclSuccess) return KNN_ERR_RCCL;
@@ -402,6 +455,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
                               d[g].comm, d[g].cs) != ncclSuccess)
                 rc = KNN_ERR_RCCL;
         if (ncclGroupEnd() != ncclSuccess && !rc) rc = KNN_ERR_RCCL;
+        if (!rc) rc = ring_drain(d, P, &tr, 0, &aborted);
         if (!rc && (hipSetDevice(d[0].dev) != hipSuccess ||
                     hipMemcpyAsync(hm, d[0].meta, sizeof(hm), hipMemcpyDeviceToHost, d[0].cs) != hipSuccess ||
                     hipStreamSynchronize(d[0].cs) != hipSuccess))
@@ -444,6 +498,9 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         rc = direct_pass(d, P, R, m, n, dtype, 0, form, &tr);
     else if (!rc)
         rc = ring_pass(d, P, R, m, form ? knn_ctx_shadow_bytes(d[0].ctx, R) : bytes, 0, 0, form, &tr);
+    /* every transfer of the pass has landed (or the search fails here):
+     * knn_ctx_end's synchronisation can then not wait on a stuck hop */
+    if (!rc && P > 1) rc = ring_drain(d, P, &tr, 1, &aborted);
     size_t unresolved_total = 0;
     for (int g = 0; g < P && !rc; g++) {
         size_t u = 0;
@@ -475,6 +532,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         } else if (!rc) {
             rc = ring_pass(d, P, R, m, bytes, P - 1, 1, 0, &tr);
         }
+        if (!rc && P > 1) rc = ring_drain(d, P, &tr, 1, &aborted);
         for (int g = 0; g < P && !rc; g++) {
             hipSetDevice(d[g].dev);
             rc = knn_ctx_rescan_end(d[g].ctx, d[g].d_out, d[g].cs);
@@ -490,7 +548,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             rc = KNN_ERR_HIP;
     }
 
-    for (int g = 0; g < P; g++) {
+    for (int g = 0; g < P && !aborted; g++) {
         hipSetDevice(d[g].dev);
         if (d[g].cs) hipStreamSynchronize(d[g].cs);
         if (d[g].ms) hipStreamSynchronize(d[g].ms);
@@ -510,7 +568,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         if (d[g].ev_comm) hipEventDestroy(d[g].ev_comm);
         if (d[g].cs) hipStreamDestroy(d[g].cs);
         if (d[g].ms) hipStreamDestroy(d[g].ms);
-        if (tr.kind == RING_RCCL && comms[g]) ncclCommDestroy(comms[g]);
+        if (tr.kind == RING_RCCL && comms[g] && !aborted) ncclCommDestroy(comms[g]);
     }
     if (tr.fabric) hipStreamDestroy(tr.fabric);
     return rc;

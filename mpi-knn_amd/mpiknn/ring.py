@@ -34,8 +34,48 @@ mpi-knn-parallel_blocking.c:122-244 / _non_blocking.c:132-259:
 The engine object does the per-block work (GpuEngine: libknn kernels on the
 current HIP stream).  Tests substitute a CPU engine to check the schedule
 under gloo.
+
+Failures: a peer that dies or stalls must not hang the survivors.  Every
+exchange is waited for with a bound (KNN_RING_TIMEOUT_S, default 300 s; a
+full-size P = 8 pass moves ~50 MB a rank and takes milliseconds): under gloo
+each request's wait carries that timeout; under nccl (RCCL) the wait stays
+a stream-ordered one -- a host-blocking wait would stall the launch queue
+behind the transfers -- and the bound is the process group's own timeout,
+which bench.py sets from the same variable at init_process_group (the RCCL
+watchdog aborts the communicator when it expires).  Either way the caller
+gets RingError, not a hang (tests/test_ring_cpu.py injects a stalled peer).
 """
+import datetime
+import os
+
 import numpy as np
+
+
+class RingError(RuntimeError):
+    """A block exchange of the ring failed or timed out on this rank."""
+
+
+def ring_timeout_s():
+    """The bound on one exchange (KNN_RING_TIMEOUT_S, seconds; default 300)."""
+    return float(os.environ.get("KNN_RING_TIMEOUT_S", "300"))
+
+
+def _wait_all(dist, reqs, rank, what, timeout_s):
+    backend = None
+    gb = getattr(dist, "get_backend", None)
+    if gb is not None:
+        try:
+            backend = gb()
+        except Exception:
+            backend = None
+    for r in reqs:
+        try:
+            if backend == "gloo":
+                r.wait(timeout=datetime.timedelta(seconds=timeout_s))
+            else:
+                r.wait()
+        except Exception as e:   # a dead or stalled peer: fail loudly, never hang
+            raise RingError("rank %d: %s failed (%s)" % (rank, what, e)) from e
 
 
 def partition(m, P):
@@ -216,7 +256,7 @@ class GpuEngine:
         return host.view(self.mk.NB_DTYPE).reshape(-1, self.k)[: self.nq]
 
 
-def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
+def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_s=None):
     """Run the ring on this rank.  `engine` holds the packed own block
     (engine.pack done).  Collective calls: all_reduce(meta), the block
     exchange of each pass, all_reduce(unresolved).  Returns the number of
@@ -232,8 +272,19 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
                 (one fused int8 launch for byte blocks, knn_ctx_step_shadow_n).
                 A ring hop carries one block over one link per step; the
                 direct exchange spreads the same bytes over all seven links of
-                an 8-GPU node in the time of one hop."""
-    import os
+                an 8-GPU node in the time of one hop.
+
+    The default is "direct": both schedules are bit-identical and run the
+    same P2P primitive (batch_isend_irecv = one RCCL group), the direct one
+    in one group of 2(P-1) operations a rank, which needs no ordering across
+    groups (tested under gloo at P = 2..8 and through the one-GPU loopback
+    at P = 2..12).  Neither has run over RCCL with P > 1 yet: set
+    KNN_RING_SCHEDULE=ring to fall back to the reference's rotation.
+
+    timeout_s bounds every exchange wait (default ring_timeout_s()); a
+    failed or stalled peer raises RingError (module docstring)."""
+    if timeout_s is None:
+        timeout_s = ring_timeout_s()
     if schedule is None:
         schedule = os.environ.get("KNN_RING_SCHEDULE", "direct")
     if schedule not in ("ring", "direct"):
@@ -317,8 +368,7 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
                 engine.step_shadow(state["cur"], rows, base)
             else:
                 engine.step(state["cur"], rows, base, rescan)
-            for r in reqs:
-                r.wait()
+            _wait_all(dist, reqs, rank, "ring hop %d" % s, timeout_s)
             if s < P - 1:
                 if use_wire:
                     engine.wire_unpack(nxt, land)
@@ -369,8 +419,7 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
             engine.step_shadow(own, rows, base)
         else:
             engine.step(own, rows, base, rescan)
-        for r in reqs:
-            r.wait()
+        _wait_all(dist, reqs, rank, "direct exchange", timeout_s)
         if resident is not None:
             fold = resident
         elif use_wire:
@@ -404,7 +453,7 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None):
         # the merge end() synchronised with waits for: it has landed)
         if not engine.mk.s8_spec_ok(verify.numpy(), engine.n, engine.dtype):
             engine.spec_hint = None   # not this data: the checked path, from the start
-            return ring_search(dist, torch, engine, rank, P, m, q_base, schedule)
+            return ring_search(dist, torch, engine, rank, P, m, q_base, schedule, timeout_s)
     total = unresolved
     if P > 1:
         t = torch.tensor([float(unresolved)], dtype=torch.float64, device=engine.meta.device)

@@ -228,3 +228,55 @@ def test_int8_research_of_uncertified(knn, oracle, monkeypatch):
     if counts["off"] == 0:
         pytest.skip("no uncertified queries on this data")
     assert counts["on"] < counts["off"], counts
+
+
+@pytest.mark.parametrize("dtype,k", [("f64", 30), ("f32", 64)])
+def test_s8_speculative_mismatch_real_valued(knn, oracle, dtype, k):
+    """a speculative begin (the last search's host meta as
+    the hint) on data that turns out real-valued -- the device meta says GEMM
+    while the context holds no element rows.  k <= 32 takes the rank merge,
+    k > 32 (fp32) k_merge; neither may read through the missing element
+    block, the int8 re-search must not run, and the search is then repeated
+    from the element block: every result equal to the oracle's."""
+    import torch
+    import mpiknn.ring as ring
+    X = datasets.mnist_like(1300, 96, seed=12)[0]
+    m, n = X.shape
+    Xr = X / 255.0 + np.random.default_rng(3).normal(0, 1e-3, X.shape)
+    e = ring.GpuEngine(torch, 0, n, m, m, k, dtype=dtype)
+    for trial, Y in enumerate((X, Xr, X)):
+        e.try_s8 = True
+        Ys = Y.astype(np.float32) if dtype == "f32" else Y
+        e.pack(torch.from_numpy(np.ascontiguousarray(Ys)).to("cuda:0"), layout_col=False)
+        assert e.spec
+        ring.ring_search(None, torch, e, 0, 1, m, 0)
+        got = e.result()
+        Yr = Ys.astype(np.float64)
+        ref = oracle.knn(Yr, k)
+        assert np.array_equal(got["idx"], ref["idx"]), trial
+        assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), trial
+        # the mismatch drops the hint: the search after it reads its meta back
+        assert (e.spec_hint is not None) == (trial != 1), trial
+
+
+@pytest.mark.parametrize("kl", ["12", "17"])
+def test_int8_research_every_query_uncertified(knn, oracle, kl, monkeypatch):
+    """the int8 re-search with nf == nq -- 20 rows repeated
+    75 times, so every query's k nearest nonzero distances are a 75-way tie
+    that no lane list (12, 17 or 65 entries) can certify -- under both
+    lane-list lengths: all of them fall through to the exact rescan, exact."""
+    import torch
+    import mpiknn.ring as ring
+    monkeypatch.setenv("KNN_I8_KL", kl)
+    rng = np.random.default_rng(5)
+    X = np.repeat(rng.integers(0, 256, (20, 64)).astype(np.float64), 75, axis=0)
+    m, n = X.shape
+    e = ring.GpuEngine(torch, 0, n, m, m, 30)
+    e.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
+    unresolved = ring.ring_search(None, torch, e, 0, 1, m, 0)
+    assert e.ctx.contraction_bits() == 8
+    assert unresolved == m
+    got = e.result()
+    ref = oracle.knn(X, 30)
+    assert np.array_equal(got["idx"], ref["idx"])
+    assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64))

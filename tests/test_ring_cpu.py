@@ -145,3 +145,64 @@ def test_ring_empty_last_block_gloo(schedule, monkeypatch):
         p.join(timeout=60)
     for rank, ok, every, every_rescan, meta_ok in sorted(res):
         assert ok and every and every_rescan and meta_ok, rank
+
+
+def _stall_worker(rank, world, port, schedule, timeout_s, q):
+    """rank 0 runs ring_search; every other rank joins the meta all-reduce
+    and then stalls (never posts its exchange), as a hung or dying peer."""
+    import sys
+    import time
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(here, "..", "oracle"), os.path.join(here, "..", "mpi-knn_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import datasets
+        import oracle
+        from mpiknn.ring import RingError, partition, ring_search
+        X, _ = datasets.digits_real()
+        m, n = X.shape
+        R, blocks = partition(m, world)
+        base, rows = blocks[rank]
+        eng = CpuEngine(oracle, n, R, rows, 30, False)
+        eng.pack(torch.from_numpy(X[base:base + rows]))
+        if rank != 0:
+            dist.all_reduce(eng.meta, op=dist.ReduceOp.MAX)
+            time.sleep(timeout_s + 20)
+            q.put((rank, "stalled", 0.0))
+            return
+        t0 = time.perf_counter()
+        try:
+            ring_search(dist, torch, eng, rank, world, m, base, schedule=schedule, timeout_s=timeout_s)
+            q.put((rank, "no error", time.perf_counter() - t0))
+        except RingError as e:
+            q.put((rank, "RingError: %s" % e, time.perf_counter() - t0))
+    finally:
+        q.close()
+        q.join_thread()   # flush the result before the hard exit
+        os._exit(0)       # the stalled peers' sockets die with them
+
+
+@pytest.mark.parametrize("schedule,world", [("direct", 2), ("ring", 2), ("direct", 3)])
+def test_ring_stalled_peer_raises_within_timeout(schedule, world):
+    """a peer that stops participating after the meta
+    all-reduce must turn into RingError on the surviving rank within the
+    exchange bound (KNN_RING_TIMEOUT_S / timeout_s), not a hang."""
+    timeout_s = 4.0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stall_worker, args=(r, world, port, schedule, timeout_s, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = q.get(timeout=120)
+        assert got[0] == 0, got
+        assert got[1].startswith("RingError"), got
+        assert got[2] < timeout_s + 10.0, got
+    finally:
+        for p in procs:
+            p.kill()
+            p.join(timeout=30)
