@@ -97,22 +97,33 @@ __device__ __forceinline__ int i8_norm_pos(int r)
     return (r & ~127) + (((b * 2 + h) * 4 + j) * 4 + i);
 }
 
-// The norm word of row r is not |x'|^2 itself but the epilogue's addend
-//     K(r) = 31 - slot(r) - 32 |x'|^2,
+// A row's |x'|^2 is stored as two words (each array in i8_norm_pos order).
+// The init word
+//     IW(r) = -floor(|x'|^2 / 2)
+// is where the row's MFMA accumulators start (the C operand of a tile's
+// first K-step), so with A = q'.c' the accumulator ends at
+//     acc = A + IW = (|q'|^2 - d^2 - p) / 2,   p = |x'|^2 & 1,
+// and the epilogue filters on acc alone: 2 acc >= |q'|^2 - lim admits every
+// candidate with d^2 <= lim (and some with d^2 = lim + 1) without one VALU
+// operation per candidate.  The slot word
+//     K2(r) = 31 - slot(r) - 32 p,
 // slot(r) = 16 (b & 1) + 4 j + i: the row's position among the 32
 // accumulator registers of a pair of m-blocks (the lane's candidates in one
-// epilogue group), increasing with the row.  With A = q'.c' from the MFMA,
-//     v = 64 A + K = 32 (|q'|^2 - d^2) + (31 - slot)
-// orders the lane's candidates by (d^2, row) in ONE signed integer: the
-// lane's largest v is its nearest candidate, lowest row first on ties
+// epilogue group), increasing with the row, gives the survivors' exact key
+//     v = 64 acc + K2 = 32 (|q'|^2 - d^2) + (31 - slot),
+// which orders the lane's candidates by (d^2, row) in ONE signed integer:
+// the lane's largest v is its nearest candidate, lowest row first on ties
 // (SURVEY F1), and d^2 = |q'|^2 - (v >> 5), slot = 31 - (v & 31) come back
-// out of it.  |x'|^2 = -(K >> 5).  Ranges (n <= 896 bytes, |x'| <= 128, d^2
-// <= n 255^2): |v| < 2^31, and inside one lane (one query) the values span
-// less than 32 (n 255^2 + 1) < 2^31 (i8_next).
+// out of it.  |x'|^2 = -2 IW - (K2 >> 5) (i8_norm_of).  Ranges (n <= 896
+// bytes, |x'| <= 128, d^2 <= n 255^2): |acc| < 2^25, |v| < 2^31, and inside
+// one lane (one query) the values span less than 32 (n 255^2 + 1) < 2^31
+// (i8_next).
 __device__ __forceinline__ int i8_norm_word(int r, int nrm)
 {
     const int rr = r & 127, b = rr >> 5, w = rr & 31;
     const int slot = 16 * (b & 1) + 4 * (w >> 3) + (w & 3);
-    return 31 - slot - 32 * nrm;
+    return 31 - slot - 32 * (nrm & 1);
 }
+__device__ __forceinline__ int i8_init_word(int nrm) { return -(nrm >> 1); }
+__device__ __forceinline__ int i8_norm_of(int k2, int iw) { return -2 * iw - (k2 >> 5); }
 #endif

@@ -49,6 +49,7 @@ struct knn_ctx {
     void *qsp, *csp[KNN_PSETS];   /* split shadow rows: the queries, converted corpus blocks */
     size_t qsp_bytes, csp_bytes;
     int lpq, klx;       /* partial lists of the active kernel: lpq per query and split, klx long */
+    int i8_wgpc;        /* int8 distance workgroups a CU (2: the half-tile kernel) */
     int cus;
     /* per-step partial lists of k_dist_topk, KNN_PSETS sets used in turn
      * (step s+1's distance kernel runs while step s is merged), each
@@ -246,7 +247,7 @@ int knn_block_pack_dt(void *d_block, int dtype, size_t cap, size_t rows, size_t 
 }
 
 size_t knn_s8_block_bytes(size_t cap, size_t n) { return knn_s8_bytes(cap, n); }
-size_t knn_s8_block_meta_offset(size_t cap, size_t n) { return knn_s8_norm_offset(cap, n) + knn_rows_pad(cap) * 4; }
+size_t knn_s8_block_meta_offset(size_t cap, size_t n) { return knn_s8_meta_offset(cap, n); }
 
 int knn_block_pack_s8(void *d_sblock, int dtype, size_t cap, size_t rows, size_t n, const void *d_src,
                       int src_dtype, size_t ld, int layout, void *stream)
@@ -598,12 +599,16 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
             c->split = c->sscale > 0.f;
         }
     }
-    c->lpq = c->i8 ? (c->force_long ? 2 : knn_i8_lpq(c->kp)) : 4;
     /* int8 lane lists: 12 entries (k <= 32), 17 on request (KNN_I8_KL=17),
      * 65 in the re-search sub-context */
     c->klx = c->i8 ? (c->force_long ? KNN_I8_KL_L : knn_i8_kl(c->kp)) : c->kl;
     if (c->i8 && !c->force_long && c->klx == KNN_I8_KL_S && getenv("KNN_I8_KL") && atoi(getenv("KNN_I8_KL")) == KNN_I8_KL)
         c->klx = KNN_I8_KL;
+    /* 12-entry lists run on 64-row half tiles, two workgroups a CU (2 lists a
+     * query); KNN_I8_W8=1 keeps the 8-wave kernel on 128-row tiles (4) */
+    c->lpq = c->i8 ? (c->force_long ? 2 : (c->klx == KNN_I8_KL_S && env_on("KNN_I8_W8") ? 4 : knn_i8_lpq(c->kp, c->klx)))
+                   : 4;
+    c->i8_wgpc = c->i8 && c->klx == KNN_I8_KL_S && c->lpq == 2 ? 2 : 1;
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
      * element fragments in the kernel instead) */
     c->shadow = c->i8 ? 2 : (c->h16 && !env_on("KNN_NO_SHADOW"));
@@ -696,12 +701,12 @@ int knn_ctx_shadow_pack(knn_ctx_t *c, void *d_sblock, const void *d_block, size_
     const size_t rp = knn_rows_pad(cap);
     if (d_block == c->qblk && rp == c->q_rows_pad && c->q8) {
         /* the query block (a ring's own block): begin converted it already */
-        HIPCHK(hipMemcpyAsync(d_sblock, c->q8, knn_s8_norm_offset(cap, c->n) + rp * 4, hipMemcpyDeviceToDevice,
+        HIPCHK(hipMemcpyAsync(d_sblock, c->q8, knn_s8_meta_offset(cap, c->n), hipMemcpyDeviceToDevice,
                               (hipStream_t)stream));
     } else {
         RCHK(knn_launch_shadow8(d_sblock, d_block, c->dtype, rp, c->n, c->meta, stream));
     }
-    HIPCHK(hipMemcpyAsync((char *)d_sblock + knn_s8_norm_offset(cap, c->n) + rp * 4,
+    HIPCHK(hipMemcpyAsync((char *)d_sblock + knn_s8_meta_offset(cap, c->n),
                           (const char *)d_block + knn_block_meta_offset_dt(cap, c->n, c->dtype),
                           KNN_META_DOUBLES * sizeof(double), hipMemcpyDeviceToDevice,
                           (hipStream_t)stream));
@@ -781,7 +786,11 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     if (per > 0 && KNN_PART_BUDGET / per < (size_t)smax)
         smax = KNN_PART_BUDGET / per > 1 ? (int)(KNN_PART_BUDGET / per) : 1;
     const double wgc = c->i8 ? KNN_WG_COST_I8_KSTEPS / (double)(knn_s8_rs(c->n) / 32) : KNN_WG_COST;
-    const double mc = c->i8 ? KNN_MERGE_COST_I8 : KNN_MERGE_COST;
+    /* half-tile int8 kernel: two workgroups a CU, each at about half the
+     * rate -- the model's slots double and its tile unit (a workgroup's
+     * tile time) with them, so the merge term, priced in tile times, halves */
+    const int slots = c->cus * (c->i8 ? c->i8_wgpc : 1);
+    const double mc = (c->i8 ? KNN_MERGE_COST_I8 : KNN_MERGE_COST) / (c->i8 ? c->i8_wgpc : 1);
     /* int8 lists: at least s_min splits so that a lane list expects <= KL/3
      * of the query's k+1 nearest (lpq lists a split; the block may hold all
      * of them): one split of 17-entry lists over a whole corpus left
@@ -800,10 +809,10 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
      * and every extra split is another set of cold lane lists (emulated
      * sift P = 8 fused launch: 3 / 4 / 6 / 9 splits 38.2 / 38.9 / 40.2 /
      * 42.7 ms; the makespan model picked 9) */
-    const int short_rows = c->i8 && knn_s8_rs(c->n) / 32 <= 8 && nqb * s_min >= c->cus;
+    const int short_rows = c->i8 && knn_s8_rs(c->n) / 32 <= 8 && nqb * s_min >= slots;
     for (int s = s_min; s <= smax && !short_rows; s++) {
         if (s > s_min && ntiles / s < 4) break;
-        const double t = launch_makespan(nqb, ntiles, s, c->cus, wgc) + mc * (double)c->nq * s;
+        const double t = launch_makespan(nqb, ntiles, s, slots, wgc) + mc * (double)c->nq * s;
         if (s == s_min || t < best_t * (1.0 - 2e-3)) {
             best = s;
             best_t = t;
@@ -1091,7 +1100,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
             tab.base[0] = (int64_t)c_base;
             tab.nc[0] = (int)nc;
         }
-        RCHK(knn_launch_dist_i8(c->kp, c->klx, c->k, c->q8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
+        RCHK(knn_launch_dist_i8(c->kp, c->klx, c->lpq, c->k, c->q8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
                                 knn_rows_pad(c->block_cap), (int)c->n, nsplit, c->part_d[set],
                                 c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr, c->qsum, ds));
     } else

@@ -19,6 +19,7 @@
 #include "knn_device.h"
 
 typedef int knn_v16i __attribute__((ext_vector_type(16)));
+typedef int knn_v8i __attribute__((ext_vector_type(8)));
 
 #define I8_INF 0x7fffffff        // empty list slot / no bound
 
@@ -181,7 +182,10 @@ __global__ __launch_bounds__(256) void k_shadow8(signed char *__restrict__ dst, 
             *(u2 *)(dst + r * (size_t)rs + j0) = (u2){lo, hi};
         }
         for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-        if (lane == 0) norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, s);
+        if (lane == 0) {
+            norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, s);
+            norms[rows_pad + i8_norm_pos((int)r)] = i8_init_word(s);
+        }
     }
 }
 
@@ -258,7 +262,7 @@ __device__ __forceinline__ int i8_blk_of(const LDS_AS i8_tab_lds *tab, int t)
 // MFMA, survivor counters) were measured with the tuning
 // harness at commit 8ea8e2a; the product source carries no hooks.
 // ---------------------------------------------------------------------------
-template <int KL, int NKS, int W, int WPS, int NST, int NB>
+template <int KL, int NKS, int W, int WPS, int NST, int NB, int TM>
 __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     const signed char *__restrict__ qsh, size_t q_rows_pad, size_t q_base, int nq,
     const knn_i8_blocks_t cb, size_t c_rows_pad, int rs,
@@ -266,13 +270,24 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     int *__restrict__ part_i, double *__restrict__ part_T, int nq_pad,
     unsigned long long *__restrict__ qthr, int uj, unsigned long long *__restrict__ qsum)
 {
-    constexpr int MB = 16 / W;              // m-blocks per wave
-    constexpr int PW = 16 / W;              // DMA pieces per wave per chunk
-    constexpr int LPQ = 2 * (W / 4);        // lists per query
-    constexpr int NORM0 = NST * 16384;
-    constexpr int BUF0 = NORM0 + NST * 512; // [W][NB][64] survivor d^2, then ids
-    constexpr int XB0 = BUF0 + 2 * W * NB * 256;   // W = 8: [8][32] bound exchange (u4, v8, v16)
-    constexpr int TB0 = XB0 + (W == 8 ? 3 * 8 * 32 * 4 : 0);   // block table
+    // TM m-blocks (32 rows each) a tile: 4 (128-row tiles) or 2 (64-row
+    // half tiles: 4 waves, two workgroups a CU).  The 4 query groups of 32
+    // take RHN = W / 4 waves each, MB = TM / RHN m-blocks a wave.
+    constexpr int TR = 32 * TM;             // rows a tile
+    constexpr int RHN = W / 4;              // waves a query group (row halves)
+    constexpr int MB = TM / RHN;            // m-blocks per wave
+    constexpr int CHB = TR * 128;           // bytes a chunk (TR rows x 128 features)
+    constexpr int PW = CHB / 1024 / W;      // DMA pieces (1 KiB) per wave per chunk
+    constexpr int LPQ = 2 * RHN;            // lists per query
+    constexpr int NRB = TR * 8;             // norm ring bytes a stage: slot + init words
+    constexpr int WPW = TR / W;             // norm words a wave stages of each array
+    constexpr int NSEG = 8 * WPW;           // a wave's staged piece (both arrays)
+    constexpr int NORM0 = NST * CHB;        // norm ring: [NST][W][slot words, init words]
+    constexpr int BUF0 = NORM0 + NST * NRB; // [W][NB][64] survivor d^2, then ids
+    constexpr int XB0 = BUF0 + 2 * W * NB * 256;   // RHN = 2: [8][32] bound exchange (u4, v8, v16)
+    constexpr int TB0 = XB0 + (RHN == 2 ? 3 * 8 * 32 * 4 : 0);   // block table
+    static_assert(MB == 2 || MB == 4, "m-blocks a wave");
+    static_assert(PW == 2 || PW == 4, "DMA pieces a wave");
     constexpr int LDSB = TB0 + (int)((sizeof(i8_tab_lds) + 15) / 16 * 16);
     __shared__ __attribute__((aligned(16))) char smem[LDSB];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -283,6 +298,9 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // a query block's later splits start from the bounds its earlier ones
     // published (qthr)
     const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;
+    // the host counts 128-row tiles; this kernel's tiles hold TR rows
+    constexpr int TS = 4 / TM;
+    ntiles *= TS;
     const int tb = ntiles / nsplit, tr = ntiles - tb * nsplit;
     const int t_lo = split * tb + (split < tr ? split : tr);
     const int t_hi = t_lo + tb + (split < tr ? 1 : 0);
@@ -306,7 +324,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             qf[s] = s < nks ? v : (knn_v4i){0, 0, 0, 0};
         }
     }
-    const int qn = -(qnorms[i8_norm_pos(myq)] >> 5);   // |q'|^2 (i8_norm_word)
+    const int qn = i8_norm_of(qnorms[i8_norm_pos(myq)], qnorms[q_rows_pad + i8_norm_pos(myq)]);   // |q'|^2
     // shared per-query bound across splits and ring steps (qthr: bits of a
     // non-negative double, atomicMin).  INT-mode bounds are integers, or the
     // next double above one (strict publication), so floor() is the int bound.
@@ -346,10 +364,10 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             tab->nc[j] = cb.nc[j];
         }
 #pragma unroll
-        for (int j = 0; j <= KNN_I8_MAXBLK; j++) tab->t0[j] = cb.t0[j];
+        for (int j = 0; j <= KNN_I8_MAXBLK; j++) tab->t0[j] = cb.t0[j] * TS;
         tab->nblk = cb.nblk;
     }
-    if constexpr (W == 8) {
+    if constexpr (RHN == 2) {
         if (h == 0) {
 #pragma unroll
             for (int j = 0; j < 3; j++) xb[256 * j + wave_s * 32 + r32] = I8_INF;
@@ -362,7 +380,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     unsigned voff[PW];
 #pragma unroll
     for (int p = 0; p < PW; p++) {
-        const int rr = (128 / W) * wave_s + 8 * p + (lane >> 3);
+        const int rr = (TR / W) * wave_s + 8 * p + (lane >> 3);
         voff[p] = (unsigned)(rr * rs + 16 * ((lane & 7) ^ ((rr >> 1) & 7)));
     }
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
@@ -375,16 +393,20 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     const int s_t0 = i8_rfl(tab->t0[s_b]);
     int s_t1 = i8_rfl(tab->t0[s_b + 1]);
     const signed char *s_row = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]) +
-                               (size_t)(t_lo - s_t0) * 128 * rs;
-    const int *s_nrow = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]) + (size_t)(t_lo - s_t0) * 128;
+                               (size_t)(t_lo - s_t0) * TR * rs;
+    const int *s_nrow = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]) + (size_t)(t_lo - s_t0) * TR;
     auto stage = [&]() {
-        const unsigned dst = lds0 + ((unsigned)s_x % NST) * 16384u + (unsigned)wave_s * (16384u / W);
+        const unsigned dst = lds0 + ((unsigned)s_x % NST) * (unsigned)CHB + (unsigned)wave_s * (unsigned)(CHB / W);
         if constexpr (PW == 4) bglds16x4(i8_rsrc(s_row + s_coff), voff[0], voff[1], voff[2], voff[3], dst);
         else bglds16x2(i8_rsrc(s_row + s_coff), voff[0], voff[1], dst);
         if (s_x < total && s_coff == 0) {
-            if (lane < 32 / W)
-                bglds16(i8_rsrc(s_nrow + (128 / W) * wave_s), 16u * lane,
-                        lds0 + NORM0 + ((unsigned)s_t % NST) * 512u + (512u / W) * wave_s);
+            // the tile's two norm arrays in one piece a wave: lanes <
+            // WPW / 4 the slot words, the next WPW / 4 lanes the init words
+            // of the same rows (c_rows_pad words further on)
+            if (lane < WPW / 2)
+                bglds16(i8_rsrc(s_nrow + WPW * wave_s),
+                        lane < WPW / 4 ? 16u * lane : 4u * (unsigned)c_rows_pad + 16u * (lane - WPW / 4),
+                        lds0 + NORM0 + ((unsigned)s_t % NST) * (unsigned)NRB + (unsigned)NSEG * wave_s);
         }
         s_x++;
         if (s_x < total) {
@@ -397,8 +419,8 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                     s_nrow = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]);
                     s_t1 = i8_rfl(tab->t0[s_b + 1]);
                 } else {
-                    s_row += (size_t)128 * rs;
-                    s_nrow += 128;
+                    s_row += (size_t)TR * rs;
+                    s_nrow += TR;
                 }
             }
         }
@@ -409,8 +431,25 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (NST - 3)) : "memory");
     };
     // A fragments (MB m-blocks) of K-step ks of staged chunk xx
+    // norm ring: byte offset of 16-byte group v (i8_norm_pos order, 4 words)
+    // of a tile's slot words; its init words sit NSEG / 2 bytes further
+    auto nofs = [&](int v) -> int { return (v / (WPW / 4)) * NSEG + (v % (WPW / 4)) * 16; };
+    // accumulator init words of tile tt for the wave's MB m-blocks (the C
+    // operand of the tile's first K-step): 4 ds_read_b128 an m-block
+    auto rdI = [&](int tt, knn_v16i (&ini)[MB]) {
+        const LDS_AS char *p = (const LDS_AS char *)smem + NORM0 + ((unsigned)tt % NST) * NRB + NSEG / 2;
+#pragma unroll
+        for (int bb = 0; bb < MB; bb++) {
+            knn_v4i r[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) r[j] = *(const LDS_AS knn_v4i *)(p + nofs(4 * h + 8 * (MB * rh + bb) + j));
+            const knn_v8i lo = __builtin_shufflevector(r[0], r[1], 0, 1, 2, 3, 4, 5, 6, 7);
+            const knn_v8i hi = __builtin_shufflevector(r[2], r[3], 0, 1, 2, 3, 4, 5, 6, 7);
+            ini[bb] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+        }
+    };
     auto rdA = [&](int xx, int ks, knn_v4i (&a)[MB]) {
-        const LDS_AS char *p = (const LDS_AS char *)smem + ((unsigned)xx % NST) * 16384 + (MB * rh * 32 + r32) * 128 +
+        const LDS_AS char *p = (const LDS_AS char *)smem + ((unsigned)xx % NST) * CHB + (MB * rh * 32 + r32) * 128 +
                                16 * ((2 * ks + h) ^ ((r32 >> 1) & 7));
 #pragma unroll
         for (int bb = 0; bb < MB; bb++) a[bb] = *(const LDS_AS knn_v4i *)(p + bb * 4096);
@@ -435,7 +474,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // counted wait would sit it out.
     // (the 12-entry-list kernels only: the 17-entry ones have no registers
     // to spare at 28 K-steps)
-    constexpr bool SUM = W == 8 && KL == KNN_I8_KL_S;
+    // (k <= 32 kernels: the shared-bound re-read, and the summaries for the
+    // 12-entry lists; a query's LPQ lanes hold 8 / 16 rows at or below
+    // their L[S8] / L[S16])
+    constexpr bool REREAD = KL != KNN_I8_KL_L;
+    constexpr bool SUM = REREAD && KL == KNN_I8_KL_S;
+    constexpr int S8 = 8 / LPQ - 1, S16 = 16 / LPQ - 1;
     int q_pubx = -1000;
     auto qsum_publish = [&](int v8, int v16) {
         if (!SUM || qsum == nullptr || rh != 0 || h != 0 || myq >= nq) return;
@@ -461,19 +505,21 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         // T a bound on the candidates a full list drops
         int nb = lmin < u ? lmin : u;
         if (uj & (1 << 16)) nb = lmin;
-        if constexpr (W == 8) {
-            // the split's summary for the other splits: v8 / v16 = the max
-            // over the query's 4 lanes of L[1] / L[3] -- 8 / 16 rows of this
-            // split lie at or below them
+        if constexpr (RHN == 2) {
             if (h == 0) xb[wave_s * 32 + r32] = u4;
             const int pu = xb[(wave_s ^ 4) * 32 + r32];
             u4 = pu > u4 ? pu : u4;
             nb = u4 < nb ? u4 : nb;
-            if constexpr (SUM) {
-                int v8 = L[1], v16 = L[3];
-                const int v8o = __shfl_xor(v8, 32), v16o = __shfl_xor(v16, 32);
-                v8 = v8o > v8 ? v8o : v8;
-                v16 = v16o > v16 ? v16o : v16;
+        }
+        if constexpr (SUM) {
+            // the split's summary for the other splits: v8 / v16 = the max
+            // over the query's LPQ lanes of L[S8] / L[S16] -- 8 / 16 rows of
+            // this split lie at or below them
+            int v8 = L[S8], v16 = L[S16];
+            const int v8o = __shfl_xor(v8, 32), v16o = __shfl_xor(v16, 32);
+            v8 = v8o > v8 ? v8o : v8;
+            v16 = v16o > v16 ? v16o : v16;
+            if constexpr (RHN == 2) {
                 if (h == 0) {
                     xb[256 + wave_s * 32 + r32] = v8;
                     xb[512 + wave_s * 32 + r32] = v16;
@@ -481,8 +527,8 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 const int p8 = xb[256 + (wave_s ^ 4) * 32 + r32], p16 = xb[512 + (wave_s ^ 4) * 32 + r32];
                 v8 = p8 > v8 ? p8 : v8;
                 v16 = p16 > v16 ? p16 : v16;
-                qsum_publish(v8, v16);
             }
+            qsum_publish(v8, v16);
         }
         thr = nb < thr ? nb : thr;
     };
@@ -554,54 +600,80 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     long c_base = 0;
     int nc = 0, e_t0 = 0, e_t1 = 0, e_b = 0;
     // Survivors are the candidates with d^2 <= lim = min(own KL-th, shared
-    // bound), i.e. v >= T = 32 (|q'|^2 - lim) (i8_norm_word).  An empty
-    // list (lim = INF) admits every real candidate: T = 32 (|q'|^2 - DMAX)
-    // with DMAX above every d^2 (n 255^2 < DMAX); masked slots take
-    // vnone = T_open - 1, below every threshold.
+    // bound).  The accumulators started at the rows' init words, so acc =
+    // (|q'|^2 - d^2 - p) / 2 (i8_init_word): the filter 2 acc >= |q'|^2 -
+    // lim, i.e. acc >= Ta = ceil((|q'|^2 - lim) / 2), admits all of them
+    // (and rows with d^2 = lim + 1, p = 1), straight off the MFMA output.
+    // Lanes that pass build the exact keys v = 64 acc + K2 and select with
+    // v >= T = 32 (|q'|^2 - lim).  An empty list (lim = INF) admits every
+    // real candidate: Ta = INT_MIN + 1, T = 32 (|q'|^2 - DMAX) with DMAX
+    // above every d^2 (n 255^2 < DMAX); masked slots take acc = INT_MIN /
+    // v = vnone = T_open - 1, below every threshold.
     const int dmax = rs * 65025 + 1;
     const int t_open = 32 * (qn - dmax), vnone = t_open - 1;
+    constexpr int A_NONE = (int)0x80000000;
     auto thr_v = [&]() -> int {
         const int lim = L[KL - 1] < thr ? L[KL - 1] : thr;
         return lim >= dmax ? t_open : 32 * (qn - lim);
     };
+    auto thr_a = [&]() -> int {
+        const int lim = L[KL - 1] < thr ? L[KL - 1] : thr;
+        return lim >= dmax ? A_NONE + 1 : (qn - lim + 1) >> 1;
+    };
+    constexpr bool ACCF = NKS <= 8;
     auto epilogue = [&](int t, knn_v16i (&A)[MB], int xdone) {
         const int lt = t - e_t0;
-        const LDS_AS knn_v4i *cn =
-            (const LDS_AS knn_v4i *)((LDS_AS char *)smem + NORM0 + ((unsigned)t % NST) * 512) + 4 * h + 8 * MB * rh;
-        const int row0 = lt * 128 + 32 * MB * rh;
+        const LDS_AS char *cn = (const LDS_AS char *)smem + NORM0 + ((unsigned)t % NST) * NRB;
+        const int row0 = lt * TR + 32 * MB * rh;
         const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 32 * qg;
         const bool masked = (row0 + 32 * MB > nc) || (gw0 < gt0 + 32 * MB && gt0 < gw0 + 32);
         const int idb = (int)(c_base + row0) + 4 * h;
-        if constexpr (W == 8) {
+        if constexpr (REREAD) {
             if (qthr != nullptr) {
                 if (q_ready >= 0 && xdone > q_ready) qthr_apply();
                 if (q_ready < 0 && (NCH == 1 || (t & 1) == 0)) qthr_issue(s_x);   // mnist: 3.89 -> 3.84 ms (kbench8)
             }
         }
-        int T = thr_v();
         // groups of 2 m-blocks = 32 candidates a lane, lower rows first (the
         // stable tie order across groups; inside one, v orders by row)
 #pragma unroll
         for (int g = 0; g < MB / 2; g++) {
+            int a[32];
+#pragma unroll
+            for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+                for (int i = 0; i < 16; i++) a[16 * bb + i] = A[2 * g + bb][i];
+            if (masked) {   // rows past the block, and the query itself (acc > -2^25 otherwise)
+#pragma unroll
+                for (int x = 0; x < 32; x++) {
+                    const int rloc = 32 * (2 * g + (x >> 4)) + 8 * ((x >> 2) & 3) + (x & 3);
+                    if (!(row0 + rloc + 4 * h < nc && idb + rloc != gq)) a[x] = A_NONE;
+                }
+            }
+            // short rows (NKS <= 8: SIFT) -- most groups end here, late in
+            // the scan; long rows (MNIST) almost always hold a survivor in
+            // some lane of the wave (kbench8 counters), so the exact keys
+            // are built straight away
+            if constexpr (ACCF) {
+                if (__ballot(i8_max32(a) >= thr_a()) == 0ull) continue;
+            }
+            // exact keys of the group (slot words from the norm ring)
             int v[32];
 #pragma unroll
             for (int bb = 0; bb < 2; bb++)
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const knn_v4i c4 = cn[8 * (2 * g + bb) + j];
+                    const knn_v4i c4 = *(const LDS_AS knn_v4i *)(cn + nofs(4 * h + 8 * (MB * rh + 2 * g + bb) + j));
 #pragma unroll
-                    for (int i = 0; i < 4; i++)
-                        v[16 * bb + 4 * j + i] = (int)((unsigned)A[2 * g + bb][4 * j + i] * 64u + (unsigned)c4[i]);
+                    for (int i = 0; i < 4; i++) v[16 * bb + 4 * j + i] = (int)((unsigned)a[16 * bb + 4 * j + i] * 64u + (unsigned)c4[i]);
                 }
-            if (masked) {   // rows past the block, and the query itself
+            if (masked) {
 #pragma unroll
-                for (int x = 0; x < 32; x++) {
-                    const int rloc = 32 * (2 * g + (x >> 4)) + 8 * ((x >> 2) & 3) + (x & 3);
-                    if (!(row0 + rloc + 4 * h < nc && idb + rloc != gq)) v[x] = vnone;
-                }
+                for (int x = 0; x < 32; x++) v[x] = a[x] == A_NONE ? vnone : v[x];
             }
+            int T = thr_v();
             int vm = i8_max32(v);
-            if (__ballot(vm >= T) == 0ull) continue;   // common late in the scan
+            if (__ballot(vm >= T) == 0ull) continue;
             // survivors in (d^2, row) order, one a round per lane: into the
             // lane's LDS buffer (NB entries); a full buffer anywhere merges
             // the wave's buffers into the lists (dense insertion rounds)
@@ -644,11 +716,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 c_base = (long)i8_rfl64(tab->base[e_b]);
                 nc = i8_rfl(tab->nc[e_b]);
             }
+            // the tile's accumulators start at its init words (read at the
+            // tile's start, straight into the accumulator registers: held
+            // from earlier they cost 32 more VGPRs, or 16 v_mov_b64 a tile
+            // where the next tile's set is loaded beside the live one)
             knn_v16i acc[MB];
-#pragma unroll
-            for (int bb = 0; bb < MB; bb++)
-#pragma unroll
-                for (int i = 0; i < 16; i++) acc[bb][i] = 0;
+            rdI(t, acc);
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 const int kt = NKS - 4 * c < 4 ? NKS - 4 * c : 4;   // static after unrolling
@@ -666,12 +739,14 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x + 1)
                             rdA(x + 1, 0, anxt);
+                            // the next tile's norms arrived with its first
+                            // chunk: its init words load under this K-step's
+                            // MFMAs and the epilogue
                             stage();
                         }
 #pragma unroll
                         for (int bb = 0; bb < MB; bb++)
-                            acc[bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(acur[bb], qf[4 * c + ks],
-                                                                            acc[bb], 0, 0, 0);
+                            acc[bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(acur[bb], qf[4 * c + ks], acc[bb], 0, 0, 0);
 #pragma unroll
                         for (int bb = 0; bb < MB; bb++) acur[bb] = anxt[bb];
                     }
@@ -681,7 +756,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             epilogue(t, acc, x);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA left in flight
-        if constexpr (W == 8) {
+        if constexpr (REREAD) {
             if (q_ready >= 0) qthr_apply();
         }
     }
@@ -698,7 +773,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     }
     double pub = thr == I8_INF ? KNN_INF : (double)thr;
     if (lastmin > thr && thr < I8_INF) pub = nextafter((double)thr, KNN_INF);
-    if constexpr (W == 8) {
+    if constexpr (RHN == 2) {
         double *xd = (double *)((char *)smem + NORM0);   // the norm ring is free now
         __syncthreads();
         if (h == 0 && rh == 1) xd[qg * 32 + r32] = pub;
@@ -740,8 +815,9 @@ __global__ __launch_bounds__(256) void k_gather8(signed char *__restrict__ dst, 
         for (int b = 4 * lane; b < rs; b += 256)
             *(int *)(dst + r * rs + b) = q >= 0 ? *(const int *)(src + (size_t)q * rs + b) : 0;
         if (lane == 0) {
-            const int nrm = q >= 0 ? -(sn[i8_norm_pos(q)] >> 5) : 0;
+            const int nrm = q >= 0 ? i8_norm_of(sn[i8_norm_pos(q)], sn[src_rows_pad + i8_norm_pos(q)]) : 0;
             dn[i8_norm_pos((int)r)] = i8_norm_word((int)r, nrm);
+            dn[dst_rows_pad + i8_norm_pos((int)r)] = i8_init_word(nrm);
         }
     }
 }
@@ -812,19 +888,19 @@ extern "C" int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t 
     return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
 }
 
-template <int KL, int NKS, int W, int WPS, int NST, int NB>
+template <int KL, int NKS, int W, int WPS, int NST, int NB, int TM>
 static void launch_i8(dim3 grid, hipStream_t s, const void *qsh, size_t q_rows_pad, size_t q_base,
                       int nq, const knn_i8_blocks_t &cb, size_t c_rows_pad, int rs,
                       int nks, int ntiles, int nsplit, int nqb, double *part_d, int *part_i,
                       double *part_T, int nq_pad, double *qthr, int uj, unsigned long long *qsum)
 {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KL, NKS, W, WPS, NST, NB>), grid, dim3(64 * W), 0, s,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KL, NKS, W, WPS, NST, NB, TM>), grid, dim3(64 * W), 0, s,
                        (const signed char *)qsh, q_rows_pad, q_base, nq, cb, c_rows_pad, rs, nks, ntiles,
                        nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj,
-                       W == 8 ? qsum : nullptr);
+                       KL != KNN_I8_KL_L ? qsum : nullptr);
 }
 
-extern "C" int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t q_rows_pad, size_t q_base,
+extern "C" int knn_launch_dist_i8(int kp, int kl, int lpq, int k, const void *qsh, size_t q_rows_pad, size_t q_base,
                                   int nq, const knn_i8_blocks_t *cbp, size_t c_rows_pad, int n,
                                   int nsplit, double *part_d, int *part_i, double *part_T,
                                   int nq_pad, double *qthr, unsigned long long *qsum, void *stream)
@@ -857,7 +933,12 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t
     int uj = (k + 1 + 1) / 2 - 1, uj4 = (k + 1 + 3) / 4 - 1;
     const int no2 = uj > kl - 1;   // 2 lists of kl cannot hold k + 1
     if (uj > kl - 1) uj = kl - 1;
-    if (4 * kl < k + 1) return KNN_ERR_INVALID;   // the 4-lane bound needs 4 KL >= k + 1
+    // the list shapes: 4 lists of kl a query (8 waves, 128-row tiles), or 2
+    // (4-wave kernels: 65-entry lists, or 12-entry lists on 64-row tiles)
+    const int half = kl == KNN_I8_KL_S && lpq == 2;
+    if (!(lpq == 4 && (kl == KNN_I8_KL_S || kl == KNN_I8_KL)) && !(lpq == 2 && (half || kl == KNN_I8_KL_L)))
+        return KNN_ERR_INVALID;
+    if (lpq == 4 && 4 * kl < k + 1) return KNN_ERR_INVALID;   // the 4-lane bound needs 4 KL >= k + 1
     uj |= uj4 << 8;
     if (no2) uj |= 1 << 16;
     const dim3 grid((unsigned)(nqb * nsplit));
@@ -873,25 +954,36 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t
     // tools/probe/kbench8 variants);
     // k <= 128: 4 waves (one a SIMD, 4 m-blocks, 2 lists a query, 512 VGPRs).
     // K-step buckets: the smallest instantiated NKS >= nks
-    if (kl == KNN_I8_KL_S) {
+    if (half) {
+        // 12-entry lists, 64-row half tiles: 4 waves (32 queries x 2
+        // m-blocks each) and 80 KB of LDS a workgroup, so two workgroups
+        // share a CU -- each SIMD runs one wave of each, whose barriers and
+        // epilogues are independent: one's epilogue runs under the other's
+        // MFMAs (the 8-wave form's two waves a SIMD sat at the same barriers)
+        if (nks <= 4) launch_i8<KNN_I8_KL_S, 4, 4, 2, 8, 5, 2>(I8_ARGS);
+        else if (nks <= 8) launch_i8<KNN_I8_KL_S, 8, 4, 2, 8, 5, 2>(I8_ARGS);
+        else if (nks <= 16) launch_i8<KNN_I8_KL_S, 16, 4, 2, 8, 5, 2>(I8_ARGS);
+        else if (nks <= 25) launch_i8<KNN_I8_KL_S, 25, 4, 2, 8, 5, 2>(I8_ARGS);
+        else launch_i8<KNN_I8_KL_S, 28, 4, 2, 8, 5, 2>(I8_ARGS);
+    } else if (kl == KNN_I8_KL_S) {
         // 12-entry lists merge cheaply: 5-entry buffers (merging sooner)
         // against 6 -- kbench8, cold bounds: mnist 4.15 -> 3.91 ms, the P = 8
         // fused launch 0.69 -> 0.65 ms, sift 276 -> 277 ms; in bench.py and
         // the ring emulation within run-to-run noise
-        if (nks <= 4) launch_i8<KNN_I8_KL_S, 4, 8, 2, 8, 5>(I8_ARGS);
-        else if (nks <= 8) launch_i8<KNN_I8_KL_S, 8, 8, 2, 8, 5>(I8_ARGS);
-        else if (nks <= 16) launch_i8<KNN_I8_KL_S, 16, 8, 2, 8, 5>(I8_ARGS);
-        else if (nks <= 25) launch_i8<KNN_I8_KL_S, 25, 8, 2, 8, 5>(I8_ARGS);
-        else launch_i8<KNN_I8_KL_S, 28, 8, 2, 8, 5>(I8_ARGS);
+        if (nks <= 4) launch_i8<KNN_I8_KL_S, 4, 8, 2, 8, 5, 4>(I8_ARGS);
+        else if (nks <= 8) launch_i8<KNN_I8_KL_S, 8, 8, 2, 8, 5, 4>(I8_ARGS);
+        else if (nks <= 16) launch_i8<KNN_I8_KL_S, 16, 8, 2, 8, 5, 4>(I8_ARGS);
+        else if (nks <= 25) launch_i8<KNN_I8_KL_S, 25, 8, 2, 8, 5, 4>(I8_ARGS);
+        else launch_i8<KNN_I8_KL_S, 28, 8, 2, 8, 5, 4>(I8_ARGS);
     } else if (kl == KNN_I8_KL) {
-        if (nks <= 4) launch_i8<KNN_I8_KL, 4, 8, 2, 8, 6>(I8_ARGS);
-        else if (nks <= 8) launch_i8<KNN_I8_KL, 8, 8, 2, 8, 6>(I8_ARGS);
-        else if (nks <= 16) launch_i8<KNN_I8_KL, 16, 8, 2, 8, 6>(I8_ARGS);
-        else if (nks <= 25) launch_i8<KNN_I8_KL, 25, 8, 2, 8, 6>(I8_ARGS);
-        else launch_i8<KNN_I8_KL, 28, 8, 2, 8, 6>(I8_ARGS);
+        if (nks <= 4) launch_i8<KNN_I8_KL, 4, 8, 2, 8, 5, 4>(I8_ARGS);
+        else if (nks <= 8) launch_i8<KNN_I8_KL, 8, 8, 2, 8, 5, 4>(I8_ARGS);
+        else if (nks <= 16) launch_i8<KNN_I8_KL, 16, 8, 2, 8, 5, 4>(I8_ARGS);
+        else if (nks <= 25) launch_i8<KNN_I8_KL, 25, 8, 2, 8, 5, 4>(I8_ARGS);
+        else launch_i8<KNN_I8_KL, 28, 8, 2, 8, 5, 4>(I8_ARGS);
     } else if (kl == KNN_I8_KL_L) {
-        if (nks <= 4) launch_i8<KNN_I8_KL_L, 4, 4, 1, 8, 8>(I8_ARGS);
-        else launch_i8<KNN_I8_KL_L, 28, 4, 1, 8, 8>(I8_ARGS);
+        if (nks <= 4) launch_i8<KNN_I8_KL_L, 4, 4, 1, 8, 8, 4>(I8_ARGS);
+        else launch_i8<KNN_I8_KL_L, 28, 4, 1, 8, 8, 4>(I8_ARGS);
     } else {
         return KNN_ERR_INVALID;
     }

@@ -70,8 +70,10 @@ static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
 
 /* Byte block (knn_i8.hip): the int8 form of a packed block for the int8
  * MFMA contraction of 8-bit-window integer data.  Rows of knn_s8_rs(n)
- * bytes (x - o, o = 128 - meta[MAXNEG]; 0 past n), then one int32 |x - o|^2 per row in
- * the per-tile order of i8_norm_pos, then the block's 8 meta doubles. */
+ * bytes (x - o, o = 128 - meta[MAXNEG]; 0 past n), then two int32 words per
+ * row, each array in the per-tile order of i8_norm_pos: the slot/parity
+ * words (i8_norm_word), then the accumulator init words (i8_init_word,
+ * -floor(|x - o|^2 / 2)); then the block's 8 meta doubles. */
 #define KNN_I8_MAX_N 896  /* 7 chunks of 128 features: queries stay in VGPRs */
 #define KNN_I8_KL_S 12    /* per-lane list, k <= 32: 8-wave kernel, 4 lists a query  */
                           /* (4 KL >= k + 1: the 4-lane bound; no 2-lane bound)     */
@@ -80,9 +82,10 @@ static inline size_t knn_esize(int dtype) { return dtype == KNN_F32 ? 4 : 8; }
 /* row bytes: whole K-steps of 32 */
 static inline size_t knn_s8_rs(size_t n) { return knn_round_up(n ? n : 1, 32); }
 static inline size_t knn_s8_norm_offset(size_t cap, size_t n) { return knn_rows_pad(cap) * knn_s8_rs(n); }
+static inline size_t knn_s8_meta_offset(size_t cap, size_t n) { return knn_s8_norm_offset(cap, n) + knn_rows_pad(cap) * 8; }
 static inline size_t knn_s8_bytes(size_t cap, size_t n)
 {
-    return knn_round_up(knn_s8_norm_offset(cap, n) + knn_rows_pad(cap) * 4 + 8 * sizeof(double), 16);
+    return knn_round_up(knn_s8_meta_offset(cap, n) + 8 * sizeof(double), 16);
 }
 /* Corpus blocks of one k_dist_topk_i8 launch (a fused ring step): byte
  * blocks of one capacity, ascending global base (so every lane meets its
@@ -99,7 +102,10 @@ typedef struct {
     int nblk;
 } knn_i8_blocks_t;
 static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL_S : KNN_I8_KL_L; }
-static inline int knn_i8_lpq(int kp) { return kp <= KNN_KP_M ? 4 : 2; }
+/* lists per query: 2 for the 65-entry lists (k > 32) and for the 12-entry
+ * lists on 64-row half tiles (the k <= 32 default); 4 for the 8-wave
+ * kernel on 128-row tiles (17-entry lists, or KNN_I8_W8=1) */
+static inline int knn_i8_lpq(int kp, int kl) { return kp <= KNN_KP_M && kl != KNN_I8_KL_S ? 4 : 2; }
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
 {
     return knn_round_up(n ? n : 1, 128 / knn_esize(dtype));
@@ -152,7 +158,7 @@ int knn_launch_shadow_split(void *dst, const void *blk, int dtype, size_t rows_p
  * int8 distance + top-k kernel (partial lists [split][query][2][kl]) */
 int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,
                        const double *meta, void *stream);
-int knn_launch_dist_i8(int kp, int kl, int k, const void *qsh, size_t q_rows_pad, size_t q_base, int nq,
+int knn_launch_dist_i8(int kp, int kl, int lpq, int k, const void *qsh, size_t q_rows_pad, size_t q_base, int nq,
                        const knn_i8_blocks_t *cb, size_t c_rows_pad, int n, int nsplit,
                        double *part_d, int *part_i, double *part_T, int nq_pad, double *qthr,
                        unsigned long long *qsum, void *stream);

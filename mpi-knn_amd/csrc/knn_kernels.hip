@@ -307,8 +307,9 @@ template <typename T>
 __device__ __forceinline__ int knn_spec8(T v)
 {
     // x - 128 of an in-window integer; anything else gives garbage the meta
-    // rejects (clamped: no undefined conversion)
-    const T c = v < (T)-1e6 ? (T)-1e6 : (v > (T)1e6 ? (T)1e6 : v);
+    // rejects: NaN -> 0 and a clamp to [-32640, 32895], so the conversion is
+    // defined and (x - 128)^2 < 2^31 (the squares are summed as unsigned)
+    const T c = v == v ? (v < (T)-32640 ? (T)-32640 : (v > (T)32895 ? (T)32895 : v)) : (T)0;
     return (int)c - 128;
 }
 
@@ -325,7 +326,7 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
     __shared__ double part[4][64];
     __shared__ unsigned ipart[4][64];
     int *norms = (int *)(dst + rows_pad * (size_t)rs);
-    double *meta = (double *)(norms + rows_pad);
+    double *meta = (double *)(norms + 2 * rows_pad);
     const size_t i0 = (size_t)blockIdx.x * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const size_t i = i0 + tx;
@@ -370,6 +371,7 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
         const double nr = (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]);
         const unsigned ni = (ipart[0][tx] + ipart[1][tx]) + (ipart[2][tx] + ipart[3][tx]);
         norms[i8_norm_pos((int)i)] = i8_norm_word((int)i, (int)ni);
+        norms[rows_pad + i8_norm_pos((int)i)] = i8_init_word((int)ni);
         if (nr == nr) mnorm = nr;
         else ma.nonfin = 1.0;
     }
@@ -387,7 +389,7 @@ __global__ __launch_bounds__(256) void k_pack8_row(signed char *__restrict__ dst
     typedef typename std::conditional<sizeof(S) == 8, dbl2, flt4>::type svec_t;
     constexpr int SV = 16 / (int)sizeof(S);
     int *norms = (int *)(dst + rows_pad * (size_t)rs);
-    double *meta = (double *)(norms + rows_pad);
+    double *meta = (double *)(norms + 2 * rows_pad);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ng = rs / 8;
     knn_meta_acc ma;
@@ -428,7 +430,10 @@ __global__ __launch_bounds__(256) void k_pack8_row(signed char *__restrict__ dst
             s += __shfl_xor(s, off);
             si += (unsigned)__shfl_xor((int)si, off);
         }
-        if (lane == 0) norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, (int)si);
+        if (lane == 0) {
+            norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, (int)si);
+            norms[rows_pad + i8_norm_pos((int)r)] = i8_init_word((int)si);
+        }
         if (s == s) mnorm = s > mnorm ? s : mnorm;
         else ma.nonfin = 1.0;
     }
@@ -2028,7 +2033,7 @@ static int launch_pack8(signed char *dst, size_t cap, size_t rows, size_t n, con
                         hipStream_t s)
 {
     const size_t rp = knn_rows_pad(cap), rs = knn_s8_rs(n);
-    double *meta = (double *)(dst + knn_s8_norm_offset(cap, n) + rp * 4);
+    double *meta = (double *)(dst + knn_s8_meta_offset(cap, n));
     if (hipMemsetAsync(meta, 0, KNN_META_DOUBLES * sizeof(double), s) != hipSuccess) return KNN_ERR_HIP;
     if (layout == KNN_COLMAJOR) {
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_col<T, S>), dim3((unsigned)((rp + 63) / 64)), dim3(256), 0, s,

@@ -145,6 +145,52 @@ int orc_knn_rows(const double *X, size_t m, size_t n, int layout,
     return 0;
 }
 
+/* orc_knn_rows on a row-major fp32 matrix: the same scan over the values
+ * widened to double (exact), so it is orc_knn_rows of X.astype(float64)
+ * without the 8-byte copy -- the checker of the fp32 path (KNN_F32: the
+ * exact kNN of the fp32 points) at configs[4]'s 4M x 960, where that copy
+ * would be 31 GB.  Queries: the rows listed in qidx (any order, one
+ * thread each).  Stable insertion (serial:86-91). */
+int orc_knn_rows_f32(const float *X, size_t m, size_t n, const int64_t *qidx, size_t nq, int k,
+                     int nthreads, orc_nb_t *out)
+{
+    if (!X || !out || !qidx || k <= 0) return 1;
+    for (size_t q = 0; q < nq; q++)
+        if (qidx[q] < 0 || (size_t)qidx[q] >= m) return 1;
+    orc_lists_init(out, nq, k);
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+    long long nqq = (long long)nq;
+#pragma omp parallel
+    {
+        double *a = (double *)malloc(n * sizeof(double));
+#pragma omp for schedule(dynamic, 1)
+        for (long long qq = 0; qq < nqq; qq++) {        /* serial:72 */
+            if (!a) continue;
+            const size_t q = (size_t)qidx[qq];
+            orc_nb_t *L = out + (size_t)qq * (size_t)k;
+            for (size_t j = 0; j < n; j++) a[j] = (double)X[q * n + j];
+            for (size_t i = 0; i < m; i++) {            /* serial:74 */
+                const float *b = X + i * n;
+                double S = 0;
+                for (size_t j = 0; j < n; j++) {        /* serial:76-85 */
+                    double t = a[j] - (double)b[j];
+                    double t2 = t * t;
+                    S = S + t2;
+                }
+                double d = sqrt(S);
+                if ((d < L[k - 1].distance) && (d != 0)) /* serial:86 */
+                    orc_insert_stable(L, k, d, (int32_t)(i + 1), 0);
+            }
+        }
+        free(a);
+    }
+    return 0;
+}
+
 int orc_knn_block(const double *Q, size_t nq, size_t q_base,
                   const double *C, size_t nc, size_t c_base, size_t n,
                   const double *labels, int k, int nthreads, orc_nb_t *lists)

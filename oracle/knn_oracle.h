@@ -52,6 +52,11 @@ int orc_knn_rows(const double *X, size_t m, size_t n, int layout,
  * global ids start at q_base.  Ties are ordered by (distance, idx) so the
  * result does not depend on the order blocks are visited; visiting blocks in
  * increasing c_base reproduces serial:72-93 exactly. */
+/* The same (stable insertion) over a row-major fp32 matrix, widened to
+ * double element by element -- == orc_knn_rows(X as float64) -- for the
+ * query rows listed in qidx. */
+int orc_knn_rows_f32(const float *X, size_t m, size_t n, const int64_t *qidx, size_t nq, int k,
+                     int nthreads, orc_nb_t *out);
 int orc_knn_block(const double *Q, size_t nq, size_t q_base,
                   const double *C, size_t nc, size_t c_base, size_t n,
                   const double *labels, int k, int nthreads, orc_nb_t *lists);

@@ -33,6 +33,8 @@ def lib():
         p, sz, i, d = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double
         L.orc_knn_rows.argtypes = [p, sz, sz, i, p, sz, sz, i, i, i, p]
         L.orc_knn_rows.restype = i
+        L.orc_knn_rows_f32.argtypes = [p, sz, sz, p, sz, i, i, p]
+        L.orc_knn_rows_f32.restype = i
         L.orc_knn_block.argtypes = [p, sz, sz, p, sz, sz, sz, p, i, i, p]
         L.orc_knn_block.restype = i
         L.orc_lists_init.argtypes = [p, sz, i]
@@ -70,6 +72,24 @@ def knn(X, k=30, labels=None, rows=None, literal=False, nthreads=0, layout="row"
                             int(bool(literal)), nthreads, _ptr(out))
     if rc:
         raise RuntimeError("orc_knn_rows failed rc=%d" % rc)
+    return out
+
+
+def knn_f32(X, k, rows, nthreads=0):
+    """knn() of X.astype(float64) for a row-major float32 X without the
+    float64 copy (orc_knn_rows_f32; the checker of the fp32 path at
+    configs[4]'s size).  rows: (q0, nq) or a sequence of query row indices
+    (one result row each, in that order)."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    m, n = X.shape
+    if isinstance(rows, tuple) and len(rows) == 2:
+        qidx = np.arange(rows[0], rows[0] + rows[1], dtype=np.int64)
+    else:
+        qidx = np.ascontiguousarray(rows, dtype=np.int64)
+    out = np.zeros((len(qidx), k), dtype=NB_DTYPE)
+    rc = lib().orc_knn_rows_f32(_ptr(X), m, n, _ptr(qidx), len(qidx), k, nthreads, _ptr(out))
+    if rc:
+        raise RuntimeError("orc_knn_rows_f32 failed rc=%d" % rc)
     return out
 
 

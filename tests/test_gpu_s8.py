@@ -58,9 +58,13 @@ def test_s8_block_equals_shadow8(knn, src):
     r = np.arange(m)
     rr, w = r & 127, r & 31
     pos = (r & ~127) + (((rr >> 5) * 2 + ((w >> 2) & 1)) * 4 + (w >> 3)) * 4 + (w & 3)
-    na = a[rp * rs:rp * rs + 4 * rp].view(np.int32)
-    nb = b[rp * rs:rp * rs + 4 * rp].view(np.int32)
-    assert np.array_equal(na[pos], nb[pos]), "norm words differ from k_shadow8's"
+    na = a[rp * rs:rp * rs + 8 * rp].view(np.int32)
+    nb = b[rp * rs:rp * rs + 8 * rp].view(np.int32)
+    assert np.array_equal(na[pos], nb[pos]), "slot words differ from k_shadow8's"
+    assert np.array_equal(na[rp + pos], nb[rp + pos]), "init words differ from k_shadow8's"
+    # the two words hold |x'|^2 = sum (x - 128)^2 (knn_device.h: i8_norm_of)
+    nrm = ((X.astype(np.int64) - 128) ** 2).sum(1)
+    assert np.array_equal(-2 * nb[rp + pos].astype(np.int64) - (nb[pos] >> 5), nrm)
 
 
 def _engines(torch, ring, knn, X, P, k=30, dtype="f64"):
@@ -261,15 +265,16 @@ def test_s8_speculative_mismatch_real_valued(knn, oracle, dtype, k):
 
 @pytest.mark.parametrize("kl", ["12", "17"])
 def test_int8_research_every_query_uncertified(knn, oracle, kl, monkeypatch):
-    """the int8 re-search with nf == nq -- 20 rows repeated
-    75 times, so every query's k nearest nonzero distances are a 75-way tie
-    that no lane list (12, 17 or 65 entries) can certify -- under both
-    lane-list lengths: all of them fall through to the exact rescan, exact."""
+    """the int8 re-search with nf == nq -- 2 rows repeated
+    750 times, so every query's k nearest nonzero distances are a 750-way
+    tie that overflows every lane list (12, 17 or 65 entries; a list that
+    holds only tied entries cannot certify) -- under both lane-list lengths:
+    all of them fall through to the exact rescan, exact."""
     import torch
     import mpiknn.ring as ring
     monkeypatch.setenv("KNN_I8_KL", kl)
     rng = np.random.default_rng(5)
-    X = np.repeat(rng.integers(0, 256, (20, 64)).astype(np.float64), 75, axis=0)
+    X = np.repeat(rng.integers(0, 256, (2, 64)).astype(np.float64), 750, axis=0)
     m, n = X.shape
     e = ring.GpuEngine(torch, 0, n, m, m, 30)
     e.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)

@@ -80,3 +80,14 @@ def test_block_folding_any_order(oracle, P):
             c0, c1 = b * R, min(m, (b + 1) * R)
             oracle.knn_block(X[q0:q1], q0, X[c0:c1], c0, lists)
         assert np.array_equal(lists[["distance", "idx"]], full[q0:q1][["distance", "idx"]])
+
+
+def test_oracle_f32_entry_equals_f64_scan(oracle):
+    """orc_knn_rows_f32 (configs[4]'s checker, no 8-byte copy of the
+    corpus) is orc_knn_rows on the widened values, bit for bit."""
+    rng = np.random.default_rng(17)
+    X = rng.random((2500, 96)).astype(np.float32)
+    X[9] = X[4]                                    # an exact duplicate
+    a = oracle.knn_f32(X, 100, (0, 64))
+    b = oracle.knn(X.astype(np.float64), 100, rows=(0, 64))
+    assert a.tobytes() == b.tobytes()

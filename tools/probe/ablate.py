@@ -11,6 +11,10 @@ with  KB8_SO=tools/probe/abl/libkbench8_<name>.so python tools/probe/kbench8.py
   nodma        epilogue kept, staging removed (garbage keys: timing only)
   noepi_halfdma  one of each wave's two pieces a chunk (timing only)
   noepi_nowait   pieces issued, never waited for (racy: timing only)
+  count        the product kernel plus per-wave event counters (one vector
+               atomic a wave and event, lane 0): epilogue groups, groups past
+               the init-word filter, groups with exact survivors, extraction
+               rounds, list merges (kbench8.py prints them per launch)
 """
 import os
 import subprocess
@@ -28,7 +32,28 @@ SINK = ("""            { int sk = 0;
 """)
 
 
+COUNT_HDR = """__device__ unsigned long long kb8_cnt[8];
+#define KB8_COUNT 1
+#define KB8C(i) do { if ((threadIdx.x & 63) == 0) { unsigned long long one_ = 1ull; \\
+    asm volatile("global_atomic_add_x2 %0, %1, off" :: "v"(&kb8_cnt[i]), "v"(one_) : "memory"); } } while (0)
+"""
+
+
 def patch(s, name):
+    if name == "count":
+        s = COUNT_HDR + s
+        for old, new in (
+                ("            if (__ballot(i8_max32(a) >= thr_a()) == 0ull) continue;   // common late in the scan\n",
+                 "            KB8C(0);\n            if (__ballot(i8_max32(a) >= thr_a()) == 0ull) continue;\n            KB8C(1);\n"),
+                ("            if (__ballot(vm >= T) == 0ull) continue;\n",
+                 "            if (__ballot(vm >= T) == 0ull) continue;\n            KB8C(2);\n"),
+                ("            do {\n                if (vm >= T) {\n",
+                 "            do {\n                KB8C(3);\n                if (vm >= T) {\n"),
+                ("        cnt = 0;\n        refresh();\n",
+                 "        cnt = 0;\n        KB8C(4);\n        refresh();\n")):
+            assert old in s, old
+            s = s.replace(old, new)
+        return s
     if "noepi" in name:
         old = "            epilogue(t, acc, x);\n"
         assert old in s

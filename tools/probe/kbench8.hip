@@ -12,14 +12,25 @@
 #include KB8_SRC
 #include <string.h>
 
+#ifdef KB8_COUNT
+// event counters of the "count" ablation (tools/probe/ablate.py): read
+// into h[8], then zeroed
+extern "C" int kb8_counts(unsigned long long *h)
+{
+    static const unsigned long long z[8] = {0};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(kb8_cnt), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(kb8_cnt), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 __global__ void kb8_fill_inf(double *p, int n)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = __builtin_inf();
 }
 
-// variant v: (NST, NB) = {0: (7, 8), 1: (8, 6), 2: (8, 4),
-// 3: (7, 6), 4: (7, 4), 5: (8, 5) the product} at the data's K-step bucket (sift 4,
+// variant v: (NST, NB) = {0: (7, 8), 1: (8, 3), 2: (8, 4),
+// 3: (7, 6), 4: (7, 4), 5: (8, 5) the 8-wave kernel, 6: the half-tile kernel} at the data's K-step bucket (sift 4,
 // mnist 25)
 template <int NKS, int NST, int NB>
 static void kb8_go(dim3 grid, const void *qsh, size_t q_rows_pad, int nq, const void *csh, size_t c_rows_pad,
@@ -36,7 +47,29 @@ static void kb8_go(dim3 grid, const void *qsh, size_t q_rows_pad, int nq, const 
         cb.t0[b + 1] = ntiles;
     }
     cb.t0[0] = 0;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KNN_I8_KL_S, NKS, 8, 2, NST, NB>), grid, dim3(512), 0, 0,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KNN_I8_KL_S, NKS, 8, 2, NST, NB, 4>), grid, dim3(512), 0, 0,
+                       (const signed char *)qsh, q_rows_pad, (size_t)0, nq, cb, c_rows_pad, rs, nks, ntiles,
+                       nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj,
+                       (unsigned long long *)nullptr);
+}
+
+// the half-tile product kernel (4 waves, 64-row tiles, two workgroups a CU)
+template <int NKS>
+static void kb8_half(dim3 grid, const void *qsh, size_t q_rows_pad, int nq, const void *csh, size_t c_rows_pad,
+                     int nc, int rs, int nks, int ntiles, int nsplit, int nqb, double *part_d, int *part_i,
+                     double *part_T, int nq_pad, double *qthr, int uj)
+{
+    knn_i8_blocks_t cb;
+    memset(&cb, 0, sizeof(cb));
+    cb.nblk = 1;
+    for (int b = 0; b < KNN_I8_MAXBLK; b++) {
+        cb.ptr[b] = csh;
+        cb.nptr[b] = (const char *)csh + c_rows_pad * (size_t)rs;
+        cb.nc[b] = nc;
+        cb.t0[b + 1] = ntiles;
+    }
+    cb.t0[0] = 0;
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KNN_I8_KL_S, NKS, 4, 2, 8, 5, 2>), grid, dim3(256), 0, 0,
                        (const signed char *)qsh, q_rows_pad, (size_t)0, nq, cb, c_rows_pad, rs, nks, ntiles,
                        nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj,
                        (unsigned long long *)nullptr);
@@ -68,11 +101,15 @@ extern "C" float kbench8(int variant, const void *qsh, size_t q_rows_pad, int nq
                                                nsplit, nqb, part_d, part_i, part_T, nq_pad, qthr, uj)
 #define KB8V(NKS)                               \
     switch (variant) {                          \
-    case 1: KB8(NKS, 8, 6); break;              \
+    case 1: KB8(NKS, 8, 3); break;              \
     case 2: KB8(NKS, 8, 4); break;              \
     case 3: KB8(NKS, 7, 6); break;              \
     case 4: KB8(NKS, 7, 4); break;              \
     case 5: KB8(NKS, 8, 5); break;              \
+    case 6:                                     \
+        kb8_half<NKS>(grid, qsh, q_rows_pad, nq, csh, c_rows_pad, nc, rs, nks, ntiles, nsplit, nqb, part_d, \
+                      part_i, part_T, nq_pad, qthr, uj);                                                 \
+        break;                                  \
     default: KB8(NKS, 7, 8); break;             \
     }
         if (nks <= 4) {

@@ -4,7 +4,8 @@
          [--variant 0,1] [--splits 4,6] [--m M] [--keep-qthr | --ideal-qthr]
 
 Variant v selects (NST staging stages, NB survivor-buffer entries): 0 (7, 8),
-1 (8, 6), 2 (8, 4), 3 (7, 6), 4 (7, 4), 5 (8, 5) the product (12-entry lists).  Prints one JSON line per (variant,
+1 (8, 3), 2 (8, 4), 3 (7, 6), 4 (7, 4), 5 (8, 5) the 8-wave kernel, 6 the half-tile kernel (4 waves, 64-row
+tiles, two workgroups a CU; the product) (12-entry lists).  Prints one JSON line per (variant,
 splits)."""
 import argparse
 import ctypes
@@ -85,6 +86,11 @@ def main():
     L.kbench8.argtypes = [i, p, sz, i, p, sz, i, i, i, i, p, p, p, i, p, i, i]
     L.kbench8.restype = ctypes.c_float
     flop = 2.0 * nq * m * n
+    counts = getattr(L, "kb8_counts", None)   # the "count" ablation only
+    if counts is not None:
+        counts.argtypes = [p]
+        cbuf = (ctypes.c_ulonglong * 8)()
+        counts(cbuf)
     for var, splits in [(int(x), int(s)) for x in a.variant.split(",")
                         for s in (str(a.splits) if a.splits else str(splits)).split(",")]:
         ms = L.kbench8(var, sb.data_ptr(), rp, nq, sb.data_ptr(), rp, m, n, k, splits,
@@ -93,6 +99,10 @@ def main():
         rec = {"workload": a.workload, "m": m, "nq": nq, "keep_qthr": a.keep_qthr, "ideal": a.ideal_qthr,
                "variant": var, "splits": splits, "ms": ms,
                "tops": flop / (ms * 1e-3) / 1e12 if ms > 0 else None}
+        if counts is not None:
+            counts(cbuf)
+            names = ("groups", "past_acc_filter", "exact_survivors", "extract_rounds", "merges")
+            rec["per_launch"] = {nm: cbuf[j] / (a.iters + 1) for j, nm in enumerate(names)}
         print(json.dumps(rec), flush=True)
 
 
