@@ -11,7 +11,9 @@ block) -> finalize (+ exact rescan if any query needs it).
 value = m / step time (whole job).
 
 --workload mnist-real: the same shape real-valued (mnist_like / 255 + N(0,
-1e-3)), so the fp64 GEMM mode runs: v_mfma_f64 filter + exact re-rank.
+1e-3)), so the GEMM mode runs: the split-fp16 filter (S x = hi + lo, three
+fp16 MFMAs a product, fp64 accumulation) + the exact fp64 re-rank and
+certificate (KNN_NO_SPLIT=1: the fp64 MFMA filter instead).
 --workload sift: configs[3], 1M x 128 fp32 k = 32 (SIFT-like integers,
 row-major fvecs layout).  --workload gist: configs[4]'s shape, n = 960 fp32
 k = 100, with m = 500000 by default (configs[4] is 4M rows on 8 GPUs; pass
@@ -90,7 +92,7 @@ def main():
     ap.add_argument("--check", type=int, default=8, help="queries re-checked against the oracle")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--secondary-steps", type=int, default=3,
-                    help="mnist: also time the real-valued fp64 GEMM path this many steps (0: off)")
+                    help="mnist: also time the real-valued GEMM path this many steps (0: off)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -111,9 +113,9 @@ def main():
 
     res = run_workload(args.workload, args.steps, args.warmup, args, torch, dist, rank, P, local,
                        args.check, args.m, args.n, args.k)
-    # configs[1]'s real-valued form (mnist_train_svd.mat): the fp64
-    # GEMM-mode contraction (v_mfma_f64 filter + exact re-rank), timed by the
-    # same clock a few steps, reported beside the int8 headline
+    # configs[1]'s real-valued form (mnist_train_svd.mat): the
+    # GEMM-mode contraction (split-fp16 filter + exact fp64 re-rank), timed by
+    # the same clock a few steps, reported beside the int8 headline
     secondary = None
     if args.workload == "mnist" and args.secondary_steps > 0:
         secondary = run_workload("mnist-real", args.secondary_steps, 1, args, torch, dist, rank, P, local,
@@ -125,7 +127,8 @@ def main():
     out = res["line"]
     if secondary is not None:
         sl = secondary["line"]
-        out["secondary"] = {"label": "secondary: real-valued rows, fp64 MFMA GEMM mode (not the headline)",
+        out["secondary"] = {"label": "secondary: real-valued rows, GEMM mode -- split-fp16 filter + exact fp64 "
+                                     "re-rank (not the headline)",
                             "workload": sl["config"]["workload"], "value": sl["value"], "unit": sl["unit"],
                             "ms_per_step": sl["ms_per_step"], "steps": sl["steps"], "warmup": sl["warmup"],
                             "engine": sl["engine"], "check": sl["check"], "roofline": sl["roofline"]}

@@ -31,6 +31,9 @@
  *   KNN_NO_FUSE=1         fold received byte blocks one launch each
  *   KNN_NO_PAIR_FUSED=1   the own block's step keeps a merge of its own
  *                         instead of sharing the fused step's
+ *   KNN_NO_QSUM=1         int8 kernels without the cross-split summaries
+ *   KNN_I8_W8=1           12-entry int8 lists on the 8-wave kernel (128-row
+ *                         tiles) instead of the 64-row half-tile kernel
  *   KNN_NO_RANK_MERGE=1   int8 lists merged by k_merge's argmin rounds
  *                         instead of k_merge_rank
  *   KNN_FORCE_RESCAN=1    send every query through the exact rescan pass

@@ -111,7 +111,8 @@ struct knn_ctx {
      * with 65-entry lane lists and its buffers */
     double hmeta[KNN_META_DOUBLES];
     int have_hmeta;
-    int force_long;           /* this context is such a sub-context */
+    int sub_research;         /* this context is such a sub-context: 65-entry lists
+                               * over the most splits the merge takes */
     int one_block_q8;         /* the search's only step folded its own query byte block */
     size_t step0_nc, step0_cbase;
     struct knn_ctx *sub;
@@ -601,12 +602,12 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
     }
     /* int8 lane lists: 12 entries (k <= 32), 17 on request (KNN_I8_KL=17),
      * 65 in the re-search sub-context */
-    c->klx = c->i8 ? (c->force_long ? KNN_I8_KL_L : knn_i8_kl(c->kp)) : c->kl;
-    if (c->i8 && !c->force_long && c->klx == KNN_I8_KL_S && getenv("KNN_I8_KL") && atoi(getenv("KNN_I8_KL")) == KNN_I8_KL)
+    c->klx = c->i8 ? (c->sub_research ? KNN_I8_KL_L : knn_i8_kl(c->kp)) : c->kl;
+    if (c->i8 && !c->sub_research && c->klx == KNN_I8_KL_S && getenv("KNN_I8_KL") && atoi(getenv("KNN_I8_KL")) == KNN_I8_KL)
         c->klx = KNN_I8_KL;
     /* 12-entry lists run on 64-row half tiles, two workgroups a CU (2 lists a
      * query); KNN_I8_W8=1 keeps the 8-wave kernel on 128-row tiles (4) */
-    c->lpq = c->i8 ? (c->force_long ? 2 : (c->klx == KNN_I8_KL_S && env_on("KNN_I8_W8") ? 4 : knn_i8_lpq(c->kp, c->klx)))
+    c->lpq = c->i8 ? (c->sub_research ? 2 : (c->klx == KNN_I8_KL_S && env_on("KNN_I8_W8") ? 4 : knn_i8_lpq(c->kp, c->klx)))
                    : 4;
     c->i8_wgpc = c->i8 && c->klx == KNN_I8_KL_S && c->lpq == 2 ? 2 : 1;
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
@@ -777,6 +778,13 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         int s = atoi(env);
         return s > KNN_MAX_LISTS / c->lpq ? KNN_MAX_LISTS / c->lpq : s;
     }
+    /* the re-search of a few uncertified queries: one query block, so the
+     * launch's span is one workgroup's scan -- as many splits as the merge
+     * takes (lpq * splits + 1 <= 64 lists) */
+    if (c->sub_research) {
+        const int sw = KNN_MAX_LISTS / c->lpq;
+        return ntiles < sw ? (ntiles > 0 ? (int)ntiles : 1) : sw;
+    }
     for (int e = 0; e < KNN_SPLIT_CACHE; e++)
         if (c->split_cache[e].best > 0 && c->split_cache[e].nc == nc && c->split_cache[e].lpq == c->lpq &&
             c->split_cache[e].i8 == c->i8)
@@ -797,8 +805,11 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
      * ~1e-3 of the queries uncertified (a lane list held 17 of the k) */
     int s_min = 1;
     if (c->i8) {
-        const int kl = c->klx;
-        s_min = (3 * (c->k + 1) + c->lpq * kl - 1) / (c->lpq * kl);
+        /* the half-tile kernel's 2 lists a split see twice the rows a lane:
+         * it takes 5(k+1)/KL lists a query (MNIST P = 1, uncertified
+         * queries a pass: 58 at 4 splits, 2 at 6, 0 at 7; SIFT 334 at 5) */
+        const int kl = c->klx, f = c->i8_wgpc == 2 ? 5 : 3;
+        s_min = (f * (c->k + 1) + c->lpq * kl - 1) / (c->lpq * kl);
         if (s_min > smax) s_min = smax;
         if (s_min < 1) s_min = 1;
     }
@@ -1102,7 +1113,8 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
         }
         RCHK(knn_launch_dist_i8(c->kp, c->klx, c->lpq, c->k, c->q8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
                                 knn_rows_pad(c->block_cap), (int)c->n, nsplit, c->part_d[set],
-                                c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr, c->qsum, ds));
+                                c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr,
+                                env_on("KNN_NO_QSUM") ? NULL : c->qsum, ds));
     } else
         RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq,
                                   cblk, knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta,
@@ -1203,10 +1215,15 @@ int knn_ctx_shadow(const knn_ctx_t *c) { return c ? c->shadow : 0; }
 /* Uncertified queries of a single-block int8 search (P = 1: the block is
  * the query block, resident as q8) are searched again on the int8
  * contraction with 65-entry lane lists -- a lane can then only overflow if
- * more than 64 rows tie at or below the query's (k+1)-th distance -- and
- * the certified results replace the fp64 rescan for them; what stays
- * uncertified (ties beyond that) goes to the exact rescan as before.  SIFT
- * (1M x 128, k = 32): 186 queries, 8.4 ms of fp64 scan. */
+ * more than 64 rows tie at or below the query's (k+1)-th distance -- over
+ * 31 corpus splits, each query starting from the (k+1)-th key the search
+ * kept for it (k_merge_rank); the certified results replace the fp64
+ * rescan for them, and what stays uncertified goes to the exact rescan as
+ * before.  SIFT (1M x 128, k = 32): 186 queries, 8.4 ms of fp64 scan.
+ * (12-entry lists over 31 splits certified none of MNIST's: those are
+ * queries whose k-th and (k+1)-th distances tie, 35 of 60000.) */
+static int ctx_end_device(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s);
+
 static void research8_free(knn_ctx_t *c)
 {
     if (c->sub) knn_ctx_destroy(c->sub);
@@ -1226,7 +1243,7 @@ static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
      * speculative begin (knn_ctx_begin_s8 on a stale host hint) whose data
      * turned out real-valued fails every query in GEMM mode, and the
      * sub-search would run GEMM work from a context with no element rows */
-    if (c->mode != KNN_MODE_INT || !c->i8 || c->force_long || !c->one_block_q8 || c->nstep != 1 || !c->have_hmeta ||
+    if (c->mode != KNN_MODE_INT || !c->i8 || c->sub_research || !c->one_block_q8 || c->nstep != 1 || !c->have_hmeta ||
         c->step0_cbase != c->q_base || c->q_rows_pad != knn_rows_pad(c->block_cap) || c->kp > KNN_KP_M ||
         env_on("KNN_FORCE_RESCAN") || env_on("KNN_NO_RESEARCH8"))
         return KNN_OK;
@@ -1235,7 +1252,7 @@ static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
         research8_free(c);
         const size_t cap = knn_round_up((size_t)nf, KNN_TQ);
         RCHK(knn_ctx_create_dt(&c->sub, c->device, cap, c->n, c->block_cap, c->k, c->dtype));
-        c->sub->force_long = 1;
+        c->sub->sub_research = 1;
         if (hipMalloc(&c->sub_q8, knn_s8_bytes(cap, c->n)) != hipSuccess ||
             hipMalloc((void **)&c->sub_out, cap * (size_t)c->k * sizeof(knn_neighbour_t)) != hipSuccess ||
             hipMalloc((void **)&c->sub_flag, cap) != hipSuccess ||
@@ -1248,14 +1265,20 @@ static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
     knn_ctx_t *u = c->sub;
     u->nq = (size_t)nf;   /* within the capacity it was created with */
     u->nq_pad = knn_round_up((size_t)nf, KNN_TQ);
-    RCHK(knn_launch_gather8(c->sub_q8, c->q8, c->fail_list, nf, c->n, c->q_rows_pad, knn_rows_pad(c->sub_cap), s));
     /* q_base just past the block's last row id: no row is masked as "the
      * query itself" (its d^2 = 0 is dropped like every exact duplicate,
-     * serial:86) */
+     * serial:86).  Begin first (it resets the bounds), then the gather: the
+     * rows, and each query's bound -- k_merge_rank left the (k+1)-th kept
+     * key of every uncertified query in qthr, so the re-search filters with
+     * the running answer from its first tile (cold 65-entry lists admitted
+     * every row of a lane's first tiles: 682 us for two MNIST queries) */
     RCHK(ctx_begin(u, NULL, c->sub_q8, c->sub_cap, c->step0_cbase + c->step0_nc, c->meta, c->hmeta, s));
+    RCHK(knn_launch_gather8(c->sub_q8, c->q8, c->fail_list, nf, c->n, c->q_rows_pad, knn_rows_pad(c->sub_cap),
+                            c->qthr, u->qthr, s));
     RCHK(ctx_step_impl(u, NULL, c->q8, c->step0_nc, c->step0_cbase, NULL, s));
-    size_t un2 = 0;
-    RCHK(knn_ctx_end(u, c->sub_out, &un2, s));
+    /* the sub-search's fail list and count stay on the device: resolve8
+     * reads them there, so the only host read is the final count below */
+    RCHK(ctx_end_device(u, c->sub_out, s));
     RCHK(knn_launch_resolve8(c->sub_flag, c->fail_list, nf, u->fail_list, u->fail_count, c->sub_out, c->k, d_out,
                              c->fail_list2, c->fail_count, s));
     int nn = 0;
@@ -1265,6 +1288,26 @@ static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
     c->fail_list = c->fail_list2;
     c->fail_list2 = t;
     c->nfail = nn;
+    return KNN_OK;
+}
+
+/* The device side of knn_ctx_end: the last merge / finalize on the merge
+ * stream, `stream` ordered after them.  The records, the fail list and its
+ * count are then on the device; no host read (research8's sub-context). */
+static int ctx_end_device(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
+{
+    HIPCHK(hipEventRecord(c->ev_in, s));
+    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_in, 0));
+    int fin = 0;
+    RCHK(flush_pend2(c, d_out, &fin));
+    if (!fin) RCHK(merge_pending_fin(c, d_out, &fin));
+    if (!fin)
+        RCHK(knn_launch_finalize(c->dtype, c->kp, c->st_d, c->st_x, c->st_i, c->st_T, c->qblk, c->q_rows_pad,
+                                 (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
+                                 c->fail_list, c->mode_dev, c->fbound, env_on("KNN_FORCE_RESCAN"),
+                                 c->split, c->ms));
+    HIPCHK(hipEventRecord(c->ev_end, c->ms));
+    HIPCHK(hipStreamWaitEvent(s, c->ev_end, 0));
     return KNN_OK;
 }
 

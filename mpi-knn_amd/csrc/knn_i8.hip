@@ -802,12 +802,19 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
 // their own, searched again with 65-entry lane lists, and the certified
 // results scattered back.
 // ---------------------------------------------------------------------------
-// dst row i = src row list[i] (bytes and norm word; rows >= cnt zero)
+// dst row i = src row list[i] (bytes and norm words; rows >= cnt zero), and
+// the row's shared bound: dst_qthr[i] = src_qthr[list[i]] (the re-search's
+// seed, k_merge_rank)
 __global__ __launch_bounds__(256) void k_gather8(signed char *__restrict__ dst, const signed char *__restrict__ src,
                                                  const int *__restrict__ list, int cnt, int rs, size_t src_rows_pad,
-                                                 size_t dst_rows_pad)
+                                                 size_t dst_rows_pad, const unsigned long long *__restrict__ src_qthr,
+                                                 unsigned long long *__restrict__ dst_qthr)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    {
+        const int i = blockIdx.x * 256 + threadIdx.x;
+        if (i < cnt) dst_qthr[i] = src_qthr[list[i]];
+    }
     const int *sn = (const int *)(src + src_rows_pad * (size_t)rs);
     int *dn = (int *)(dst + dst_rows_pad * (size_t)rs);
     for (size_t r = (size_t)blockIdx.x * 4 + wave; r < dst_rows_pad; r += (size_t)gridDim.x * 4) {
@@ -845,12 +852,15 @@ __global__ void k_resolve8(const unsigned char *__restrict__ flag, const int *__
 }
 
 extern "C" int knn_launch_gather8(void *dst, const void *src, const int *list, int cnt, size_t n,
-                                  size_t src_rows_pad, size_t dst_rows_pad, void *stream)
+                                  size_t src_rows_pad, size_t dst_rows_pad, const double *src_qthr,
+                                  double *dst_qthr, void *stream)
 {
     const int rs = (int)knn_s8_rs(n);
-    const unsigned grid = (unsigned)((dst_rows_pad + 3) / 4 < 1024 ? (dst_rows_pad + 3) / 4 : 1024);
+    unsigned grid = (unsigned)((dst_rows_pad + 3) / 4 < 1024 ? (dst_rows_pad + 3) / 4 : 1024);
+    if (grid * 256u < (unsigned)cnt) grid = (unsigned)((cnt + 255) / 256);
     hipLaunchKernelGGL(k_gather8, dim3(grid), dim3(256), 0, (hipStream_t)stream, (signed char *)dst,
-                       (const signed char *)src, list, cnt, rs, src_rows_pad, dst_rows_pad);
+                       (const signed char *)src, list, cnt, rs, src_rows_pad, dst_rows_pad,
+                       (const unsigned long long *)src_qthr, (unsigned long long *)dst_qthr);
     return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
 }
 

@@ -132,7 +132,7 @@ int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, si
 int knn_launch_fill_inf(double *p, int count, void *stream);
 /* int8 re-search of uncertified queries (knn_i8.hip) */
 int knn_launch_gather8(void *dst, const void *src, const int *list, int cnt, size_t n, size_t src_rows_pad,
-                       size_t dst_rows_pad, void *stream);
+                       size_t dst_rows_pad, const double *src_qthr, double *dst_qthr, void *stream);
 int knn_launch_resolve8(unsigned char *flag, const int *list, int cnt, const int *sub_fail, const int *sub_cnt,
                         const knn_neighbour_t *sub_out, int k, knn_neighbour_t *out, int *new_list, int *new_cnt,
                         void *stream);

@@ -127,28 +127,37 @@ __device__ __forceinline__ int knn_mode(const double *meta, int n)
 // Reference-order exact squared distance: S = S + (a-b)^2 over j = 0..n-1,
 // two roundings per feature, no FMA (knn-serial.c:76-85; pow(x,2) -> x*x),
 // in fp64 on the block's values (fp32 blocks: the fp32-rounded inputs).
-// Read 16 bytes at a time: rows are zero padded to n_pad (a multiple of 16
-// bytes) and S + (0-0)^2 = S, so running the loop to a whole 16 B leaves S
-// bit-identical.
+// Rows are zero padded to n_pad (a multiple of 128 bytes) and S + (0-0)^2 =
+// S, so the loop runs over whole 128-byte pieces, S bit-identical.  The sum
+// is one dependent chain, and each lane's candidate row is its own gather:
+// 8 pieces of 16 bytes of both rows are loaded before any is used (16 loads
+// in flight a lane), so the chain waits on one memory latency every 128
+// bytes instead of every 16 (k_merge's re-rank was latency-bound on those
+// loads).
 template <typename T>
 __device__ __forceinline__ double knn_exact_sq_v(const T *__restrict__ a, const T *__restrict__ b,
-                                                 int n)
+                                                 int n_pad)
 {
 #pragma clang fp contract(off)
     typedef typename std::conditional<sizeof(T) == 8, dbl2, flt4>::type vec_t;
-    constexpr int V = 16 / (int)sizeof(T);
-    const int nr = (n + V - 1) / V;
+    constexpr int V = 16 / (int)sizeof(T), U = 8;
+    const int nr = n_pad / V;   // a multiple of U (n_pad: 128-byte rows)
     double S = 0.0;
-#pragma unroll 2
-    for (int p = 0; p < nr; p++) {
-        const vec_t va = ((const vec_t *)a)[p];
-        const vec_t vb = ((const vec_t *)b)[p];
+    for (int p = 0; p < nr; p += U) {
+        vec_t va[U], vb[U];
 #pragma unroll
-        for (int e = 0; e < V; e++) {
-            const double t = (double)va[e] - (double)vb[e];
-            const double t2 = t * t;
-            S = S + t2;
+        for (int u = 0; u < U; u++) {
+            va[u] = ((const vec_t *)a)[p + u];
+            vb[u] = ((const vec_t *)b)[p + u];
         }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int e = 0; e < V; e++) {
+                const double t = (double)va[u][e] - (double)vb[u][e];
+                const double t2 = t * t;
+                S = S + t2;
+            }
     }
     return S;
 }
@@ -1349,7 +1358,7 @@ __global__ __launch_bounds__(256) void k_merge(
                 sx[x] = st_x[(size_t)q * KP + spos[x]];
             } else if (exact_ok && sd[x] <= win) {
                 const int row = (int)((long)si[x] - (long)c_base);
-                sx[x] = knn_exact_sq_v<TE>(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n);
+                sx[x] = knn_exact_sq_v<TE>(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n_pad);
             } else {
                 sx[x] = KNN_INF;
             }
@@ -1496,6 +1505,7 @@ __global__ __launch_bounds__(256) void k_merge_rank(
         }
     }
     double tau = KNN_INF;   // fin: the k-th kept d^2
+    double tk1 = KNN_INF;   // fin: the (k+1)-th, the seed of an uncertified query's re-search
     for (int b0 = 0; b0 < C; b0 += 64) {
         const int my = b0 + lane;
         const unsigned long long x = my < C ? buf[my] : ~0ull;
@@ -1530,6 +1540,8 @@ __global__ __launch_bounds__(256) void k_merge_rank(
         if (emit) {
             const unsigned long long at = __ballot(my < C && r == k - 1);
             if (at) tau = (double)(unsigned)(__shfl(x, __builtin_ctzll(at)) >> 32);
+            const unsigned long long a1 = __ballot(my < C && r == k);
+            if (a1) tk1 = (double)(unsigned)(__shfl(x, __builtin_ctzll(a1)) >> 32);
         }
     }
     if (emit) {
@@ -1540,6 +1552,11 @@ __global__ __launch_bounds__(256) void k_merge_rank(
         if (!ok && lane == 0) {
             fa.fail_list[atomicAdd(fa.fail_count, 1)] = q;
             fa.fbound[q] = (fa.force_fail || mode != KNN_MODE_INT) ? KNN_INF : sqrt(tau);
+            // k + 1 distinct rows lie at or below the (k+1)-th kept key: a
+            // valid bound for the int8 re-search to start from (knn_engine.c
+            // research8; INT mode only, the search is over)
+            if (mode == KNN_MODE_INT && !fa.force_fail)
+                qthr[q] = (unsigned long long)__double_as_longlong(sizeof(TE) == 4 ? (double)__double2float_ru(tk1) : tk1);
         }
         return;
     }
@@ -1754,7 +1771,10 @@ __global__ __launch_bounds__(256) void k_rescan_step(
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int slot0 = blockIdx.x * 16 + wave * QW;
     if (slot0 >= nfail) return;                       // wave-uniform
-    const int nr = (n + V - 1) / V;                   // 16-byte pieces per row
+    // 16-byte pieces per row, whole 128-byte pieces: rows are zero padded to
+    // n_pad (query and corpus blocks alike) and S + (0-0)^2 = S
+    constexpr int U = 8;
+    const int nr = n_pad / V;
     // corpus chunk blockIdx.y: rows [row0, row1) into its own list set
     const int row0 = blockIdx.y * rows_per_chunk;
     const int row1 = min(nc, row0 + rows_per_chunk);
@@ -1802,19 +1822,24 @@ __global__ __launch_bounds__(256) void k_rescan_step(
         for (int row = row0 + lane; row < row1; row += 64) {
             const vec_t *cr = (const vec_t *)(cblk + (size_t)row * n_pad);
             double S[QW] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 2
-            for (int p = 0; p < nr; p++) {
-                const vec_t c = cr[p];
+            // 8 pieces of the row in flight before any is used (the sums are
+            // dependent chains; one memory latency every 128 bytes, not 16)
+            for (int p = 0; p < nr; p += U) {
+                vec_t c[U];
 #pragma unroll
-                for (int x = 0; x < QW; x++) {
-                    const vec_t a = ((const vec_t *)qp[x])[p];
+                for (int u = 0; u < U; u++) c[u] = cr[p + u];
 #pragma unroll
-                    for (int e = 0; e < V; e++) {
-                        const double t = (double)a[e] - (double)c[e];
-                        const double t2 = t * t;
-                        S[x] = S[x] + t2;
+                for (int u = 0; u < U; u++)
+#pragma unroll
+                    for (int x = 0; x < QW; x++) {
+                        const vec_t a = ((const vec_t *)qp[x])[p + u];
+#pragma unroll
+                        for (int e = 0; e < V; e++) {
+                            const double t = (double)a[e] - (double)c[u][e];
+                            const double t2 = t * t;
+                            S[x] = S[x] + t2;
+                        }
                     }
-                }
             }
             const int id = (int)(c_base + row);
 #pragma unroll

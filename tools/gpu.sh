@@ -6,7 +6,9 @@
 # Steps (outputs under gpurun_out/<tag>/):
 #   tests[:EXPR]          pytest -m gpu (optionally -k EXPR); then smoke()
 #   bench:WL[:STEPS]      bench.py --workload WL (CPU leg included)
-#   trace:WL              rocprofv3 --kernel-trace --stats of a bench run
+#   trace:WL[:STEPS]      rocprofv3 --kernel-trace --stats of a bench run (6 warm-up
+#                         steps inside the traced process; make_profiles.py
+#                         averages the launches after them)
 #   pmc:WL:REP            FETCH_SIZE, WRITE_SIZE, MFMA-busy passes (REP
 #                         repetitions of each, one counter group per run)
 #   emu:WL[:RANKS[:STEPS[:FUSE[:SPLITS]]]] tools/ring_emulate.py (per-rank ring
@@ -42,7 +44,7 @@ run_step() {
   trace)
     (cd /tmp && export TMPDIR=/tmp && cd "$ROOT" &&
      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/trace_$a" -o run -- \
-       python3 bench.py --workload "$a" --no-cpu-baseline --secondary-steps 0 --check 0 --steps 5 --warmup 2 \
+       python3 bench.py --workload "$a" --no-cpu-baseline --secondary-steps 0 --check 0 --steps ${b:-10} --warmup 6 \
        > "gpurun_out/trace_$a.log" 2>&1) || fail "$spec" $? ;;
   pmc)
     local rep=${b:-3} i g

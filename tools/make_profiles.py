@@ -45,11 +45,59 @@ def dominant(d):
     return ks[0] if ks else None
 
 
+def steady(trace_dir, bench_line):
+    """The traced bench run's distance-kernel launches after its warm-up
+    steps (rocprofv3 kernel_trace.csv), against the HIP-event kernel time the
+    same process reported (roofline.avg_launch_ms): the roofline fraction
+    recomputed from the committed trace, and the step time it sits under."""
+    fs = glob.glob(os.path.join(trace_dir, "**", "*kernel_trace.csv"), recursive=True)
+    if not fs or bench_line is None:
+        return None
+    rows = []
+    for f in fs:
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            if k.startswith("k_dist_topk"):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k))
+    if not rows:
+        return None
+    # the search's own instantiation (the int8 re-search of uncertified
+    # queries launches a 65-entry-list one beside it)
+    names = [k for _, _, k in rows]
+    main_k = max(set(names), key=names.count)
+    rows = sorted(r for r in rows if r[2] == main_k)
+    ro = bench_line["roofline"]
+    steps, warm, prof = bench_line["steps"], bench_line["warmup"], ro["profiled_steps"]
+    per_step = max(1, len(rows) // (warm + steps + prof))
+    keep = rows[warm * per_step:]              # timed + profiled steps
+    durs = [(e - b) * 1e-6 for b, e, _ in keep]
+    cfg = bench_line["config"]
+    flop = 2.0 * cfg["m"] * cfg["m"] * cfg["n"]
+    avg = statistics.mean(durs)
+    return {"kernel": keep[0][2], "launches_all": len(rows), "launches_steady": len(keep),
+            "warmup_steps_skipped": warm, "rocprof_steady_avg_ms": avg, "rocprof_steady_min_ms": min(durs),
+            "rocprof_steady_max_ms": max(durs),
+            "rocprof_all_avg_ms": statistics.mean([(e - b) * 1e-6 for b, e, _ in rows]),
+            "hip_event_avg_launch_ms": ro["avg_launch_ms"], "ms_per_step": bench_line["ms_per_step"],
+            "frac_hip_events": ro["frac"], "peak_tops": ro["peak"],
+            "frac_rocprof_steady": flop / (avg * 1e-3) / 1e12 / ro["peak"],
+            "note": "one process: bench.py --steps %d --warmup %d under rocprofv3 --kernel-trace; the "
+                    "first %d steps' launches dropped" % (steps, warm, warm)}
+
+
 def main():
     os.makedirs(DST, exist_ok=True)
     stats = glob.glob(os.path.join(OUT, "trace_" + WL, "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(DST, "%s_%s_kernel_stats.csv" % (TAG, WL)))
+    tl = os.path.join(OUT, "trace_%s.log" % WL)
+    tline = None
+    if os.path.exists(tl):
+        ls = [l for l in open(tl) if l.startswith("{")]
+        tline = json.loads(ls[-1]) if ls else None
+    st = steady(os.path.join(OUT, "trace_" + WL), tline)
+    if st:
+        json.dump(st, open(os.path.join(DST, "%s_%s_roofline.json" % (TAG, WL)), "w"), indent=1)
     bench = [l for l in open(os.path.join(OUT, "bench_%s.log" % WL)) if l.startswith("{")][-1]
     bench = json.loads(bench)
     m, n, dt = bench["config"]["m"], bench["config"]["n"], bench["dtype"]
@@ -97,6 +145,16 @@ def main():
                "| FETCH_SIZE x2 | %.4g | %.4g | %.4g |" % (rec["fetch_bytes"], min(fetch), max(fetch)),
                "| WRITE_SIZE | %.4g | %.4g | %.4g |" % (rec["write_bytes"], min(write), max(write)),
                "| algorithmic (corpus bytes) | %.4g | | |" % rec["algorithmic_bytes_per_launch"], ""]
+    if st:
+        md += ["## Roofline from the committed trace (%s_%s_roofline.json)" % (TAG, WL), "",
+               "| | ms | fraction of the %g TOPS peak |" % st["peak_tops"], "|---|---|---|",
+               "| rocprofv3, steady launches (%d, after %d warm-up steps) | %.4f | %.4f |"
+               % (st["launches_steady"], st["warmup_steps_skipped"], st["rocprof_steady_avg_ms"],
+                  st["frac_rocprof_steady"]),
+               "| HIP events, same process (bench.py roofline) | %.4f | %.4f |"
+               % (st["hip_event_avg_launch_ms"], st["frac_hip_events"]),
+               "| rocprofv3, every launch incl. warm-up | %.4f | |" % st["rocprof_all_avg_ms"],
+               "| bench step (ms_per_step, same process) | %.4f | |" % st["ms_per_step"], ""]
     if busy:
         mb = [b["mfma_busy"] for b in busy if b["mfma_busy"] is not None]
         wa = [b["wait_any"] for b in busy]

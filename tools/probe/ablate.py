@@ -12,9 +12,10 @@ with  KB8_SO=tools/probe/abl/libkbench8_<name>.so python tools/probe/kbench8.py
   noepi_halfdma  one of each wave's two pieces a chunk (timing only)
   noepi_nowait   pieces issued, never waited for (racy: timing only)
   count        the product kernel plus per-wave event counters (one vector
-               atomic a wave and event, lane 0): epilogue groups, groups past
-               the init-word filter, groups with exact survivors, extraction
-               rounds, list merges (kbench8.py prints them per launch)
+               atomic a wave and event, lane 0): groups past the init-word
+               filter (all groups where it is off), groups whose exact keys
+               were built, groups with exact survivors, extraction rounds,
+               list merges (kbench8.py prints them per launch)
 """
 import os
 import subprocess
@@ -43,8 +44,10 @@ def patch(s, name):
     if name == "count":
         s = COUNT_HDR + s
         for old, new in (
-                ("            if (__ballot(i8_max32(a) >= thr_a()) == 0ull) continue;   // common late in the scan\n",
-                 "            KB8C(0);\n            if (__ballot(i8_max32(a) >= thr_a()) == 0ull) continue;\n            KB8C(1);\n"),
+                ("            // exact keys of the group (slot words from the norm ring)\n",
+                 "            KB8C(0);\n            // exact keys of the group (slot words from the norm ring)\n"),
+                ("            int T = thr_v();\n            int vm = i8_max32(v);\n",
+                 "            KB8C(1);\n            int T = thr_v();\n            int vm = i8_max32(v);\n"),
                 ("            if (__ballot(vm >= T) == 0ull) continue;\n",
                  "            if (__ballot(vm >= T) == 0ull) continue;\n            KB8C(2);\n"),
                 ("            do {\n                if (vm >= T) {\n",

@@ -101,7 +101,7 @@ def main():
                "tops": flop / (ms * 1e-3) / 1e12 if ms > 0 else None}
         if counts is not None:
             counts(cbuf)
-            names = ("groups", "past_acc_filter", "exact_survivors", "extract_rounds", "merges")
+            names = ("past_acc_filter", "keys_built", "exact_survivors", "extract_rounds", "merges")
             rec["per_launch"] = {nm: cbuf[j] / (a.iters + 1) for j, nm in enumerate(names)}
         print(json.dumps(rec), flush=True)
 
