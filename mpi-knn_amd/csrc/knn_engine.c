@@ -774,16 +774,16 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     const char *env = getenv("KNN_SPLITS");
     const long nqb = (long)((c->nq + KNN_TQ - 1) / KNN_TQ);
     const long ntiles = (long)((nc + KNN_TC - 1) / KNN_TC);
-    if (env && atoi(env) > 0) {
-        int s = atoi(env);
-        return s > KNN_MAX_LISTS / c->lpq ? KNN_MAX_LISTS / c->lpq : s;
-    }
     /* the re-search of a few uncertified queries: one query block, so the
      * launch's span is one workgroup's scan -- as many splits as the merge
      * takes (lpq * splits + 1 <= 64 lists) */
     if (c->sub_research) {
         const int sw = KNN_MAX_LISTS / c->lpq;
         return ntiles < sw ? (ntiles > 0 ? (int)ntiles : 1) : sw;
+    }
+    if (env && atoi(env) > 0) {   /* (the search's splits, not the re-search's) */
+        int s = atoi(env);
+        return s > KNN_MAX_LISTS / c->lpq ? KNN_MAX_LISTS / c->lpq : s;
     }
     for (int e = 0; e < KNN_SPLIT_CACHE; e++)
         if (c->split_cache[e].best > 0 && c->split_cache[e].nc == nc && c->split_cache[e].lpq == c->lpq &&
@@ -805,10 +805,10 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
      * ~1e-3 of the queries uncertified (a lane list held 17 of the k) */
     int s_min = 1;
     if (c->i8) {
-        /* the half-tile kernel's 2 lists a split see twice the rows a lane:
+        /* the half-tile kernel's 2 lists a split see twice the rows a lane (long rows):
          * it takes 5(k+1)/KL lists a query (MNIST P = 1, uncertified
          * queries a pass: 58 at 4 splits, 2 at 6, 0 at 7; SIFT 334 at 5) */
-        const int kl = c->klx, f = c->i8_wgpc == 2 ? 5 : 3;
+        const int kl = c->klx, f = (c->i8_wgpc == 2 && knn_s8_rs(c->n) / 32 > 8) ? 5 : 3;
         s_min = (f * (c->k + 1) + c->lpq * kl - 1) / (c->lpq * kl);
         if (s_min > smax) s_min = smax;
         if (s_min < 1) s_min = 1;
@@ -821,6 +821,22 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
      * sift P = 8 fused launch: 3 / 4 / 6 / 9 splits 38.2 / 38.9 / 40.2 /
      * 42.7 ms; the makespan model picked 9) */
     const int short_rows = c->i8 && knn_s8_rs(c->n) / 32 <= 8 && nqb * s_min >= slots;
+    /* half-tile kernel, long rows, a grid of several rounds at s_min: s_min.
+     * Measured (MNIST P = 1, kernel / step ms): 7 splits 3.17 / 3.47, 12
+     * splits 3.18 / 3.55 -- the makespan model's tail estimate (12 ahead of
+     * 7) does not hold with two workgroups a CU, and every split adds merge
+     * work and a set of cold lists.  A single round (a ring rank's fused
+     * launch) still takes the model: P = 8 6 / 7 / 8 splits 0.75 / 0.69 /
+     * 0.67 ms a rank, the model's 8 */
+    if (c->i8 && c->i8_wgpc == 2 && !short_rows && nqb * s_min >= slots) {
+        best = s_min;
+        const int e = c->split_next++ % KNN_SPLIT_CACHE;
+        c->split_cache[e].nc = nc;
+        c->split_cache[e].lpq = c->lpq;
+        c->split_cache[e].i8 = c->i8;
+        c->split_cache[e].best = best;
+        return best;
+    }
     for (int s = s_min; s <= smax && !short_rows; s++) {
         if (s > s_min && ntiles / s < 4) break;
         const double t = launch_makespan(nqb, ntiles, s, slots, wgc) + mc * (double)c->nq * s;

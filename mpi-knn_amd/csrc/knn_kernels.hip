@@ -1549,6 +1549,51 @@ __global__ __launch_bounds__(256) void k_merge_rank(
         // candidate is tau; a candidate a lane turned away has d^2 >= T, and
         // with d^2 == T it may precede the k-th by index: certify tau < T
         const bool ok = mode == KNN_MODE_INT && !fa.force_fail && (T == KNN_INF || (C >= k && tau < T));
+        if (!ok && C < k + 1 && mode == KNN_MODE_INT && !fa.force_fail) {
+            // fewer than k + 1 entries under the shared bound: the k-th and
+            // (k+1)-th over every entry of the lists and the state -- still
+            // bounds on the query's k-th / (k+1)-th over all rows, which the
+            // rescan (fbound) and the int8 re-search (qthr) start from; with
+            // +inf instead they scanned cold (2.8 ms of k_rescan_step for two
+            // MNIST queries)
+            int c2 = 0;
+            if (lane < nl) {
+                const int s = lane / lpq, g = lane - s * lpq;
+                const size_t base = (((size_t)s * nq_pad + q) * lpq + g) * KL;
+#pragma unroll
+                for (int e = 0; e < KL; e++) {
+                    d[e] = part_d[base + e];
+                    id[e] = part_i[base + e];
+                    c2 += d[e] < KNN_INF ? 1 : 0;   // a prefix
+                }
+            }
+            const int cs2 = (!first_step && lane < KP && siv >= 0 && sdv < KNN_INF) ? 1 : 0;
+            const int ct2 = c2 + cs2;
+            int pre2 = 0, C2 = 0;
+#pragma unroll
+            for (int b = 0; b < 5; b++) {
+                const unsigned long long m = __ballot((ct2 >> b) & 1);
+                pre2 += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << b;
+                C2 += __popcll(m) << b;
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int e = 0; e < KL; e++)
+                if (e < c2) buf[pre2 + e] = ((unsigned long long)(unsigned)d[e] << 32) | (unsigned)id[e];
+            if (cs2) buf[pre2 + c2] = ((unsigned long long)(unsigned)sdv << 32) | (unsigned)siv;
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int b0 = 0; b0 < C2; b0 += 64) {
+                const int my = b0 + lane;
+                const unsigned long long x = my < C2 ? buf[my] : ~0ull;
+                int r = 0;
+                for (int j = 0; j < C2; j++) r += buf[j] < x ? 1 : 0;
+                const unsigned long long a0 = __ballot(my < C2 && r == k - 1);
+                if (a0) tau = (double)(unsigned)(__shfl(x, __builtin_ctzll(a0)) >> 32);
+                const unsigned long long a1 = __ballot(my < C2 && r == k);
+                if (a1) tk1 = (double)(unsigned)(__shfl(x, __builtin_ctzll(a1)) >> 32);
+            }
+        }
         if (!ok && lane == 0) {
             fa.fail_list[atomicAdd(fa.fail_count, 1)] = q;
             fa.fbound[q] = (fa.force_fail || mode != KNN_MODE_INT) ? KNN_INF : sqrt(tau);

@@ -267,21 +267,28 @@ def test_s8_speculative_mismatch_real_valued(knn, oracle, dtype, k):
 def test_int8_research_every_query_uncertified(knn, oracle, kl, monkeypatch):
     """the int8 re-search with nf == nq -- 2 rows repeated
     750 times, so every query's k nearest nonzero distances are a 750-way
-    tie that overflows every lane list (12, 17 or 65 entries; a list that
-    holds only tied entries cannot certify) -- under both lane-list lengths:
-    all of them fall through to the exact rescan, exact."""
+    tie that overflows every 12- or 17-entry lane list of the first pass (a
+    list holding only tied entries cannot certify) -- under both lane-list
+    lengths: without the re-search all of them take the exact rescan; with
+    it the 65-entry re-search over 31 splits gets nf == nq; exact either way."""
     import torch
     import mpiknn.ring as ring
     monkeypatch.setenv("KNN_I8_KL", kl)
     rng = np.random.default_rng(5)
     X = np.repeat(rng.integers(0, 256, (2, 64)).astype(np.float64), 750, axis=0)
     m, n = X.shape
-    e = ring.GpuEngine(torch, 0, n, m, m, 30)
-    e.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
-    unresolved = ring.ring_search(None, torch, e, 0, 1, m, 0)
-    assert e.ctx.contraction_bits() == 8
-    assert unresolved == m
-    got = e.result()
     ref = oracle.knn(X, 30)
-    assert np.array_equal(got["idx"], ref["idx"])
-    assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64))
+    for research in (False, True):
+        if research:
+            monkeypatch.delenv("KNN_NO_RESEARCH8", raising=False)
+        else:
+            monkeypatch.setenv("KNN_NO_RESEARCH8", "1")
+        e = ring.GpuEngine(torch, 0, n, m, m, 30)
+        e.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
+        unresolved = ring.ring_search(None, torch, e, 0, 1, m, 0)
+        assert e.ctx.contraction_bits() == 8
+        if not research:
+            assert unresolved == m     # the first pass certifies no query: the re-search gets nf == nq
+        got = e.result()
+        assert np.array_equal(got["idx"], ref["idx"]), research
+        assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), research
