@@ -63,8 +63,10 @@ def steady(trace_dir, bench_line):
         return None
     # the search's own instantiation (the int8 re-search of uncertified
     # queries launches a 65-entry-list one beside it)
-    names = [k for _, _, k in rows]
-    main_k = max(set(names), key=names.count)
+    tot = {}
+    for b, e, k in rows:
+        tot[k] = tot.get(k, 0) + (e - b)
+    main_k = max(tot, key=tot.get)   # the most time: the search's own launches
     rows = sorted(r for r in rows if r[2] == main_k)
     ro = bench_line["roofline"]
     steps, warm, prof = bench_line["steps"], bench_line["warmup"], ro["profiled_steps"]
