@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mnist")
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warm", type=int, default=3, help="untimed passes before the timed ones")
     ap.add_argument("--m", type=int, default=None)
     ap.add_argument("--splits", default=None,
                     help="comma list: repeat each P with KNN_SPLITS forced to each value (a sweep)")
@@ -149,7 +150,7 @@ def main():
                         eng.step(bufs[b], rows, base)
             return eng.end()
 
-        for _ in range(3):
+        for _ in range(args.warm):
             one()
         torch.cuda.synchronize()
         # timed without the profiling events (each event record sits on the
