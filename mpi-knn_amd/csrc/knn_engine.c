@@ -772,7 +772,9 @@ static double launch_makespan(long nqb, long ntiles, int s, int cus, double wgc)
 static int choose_splits(knn_ctx_t *c, size_t nc)
 {
     const char *env = getenv("KNN_SPLITS");
-    const long nqb = (long)((c->nq + KNN_TQ - 1) / KNN_TQ);
+    /* (workgroups of 128 qg queries: knn_i8_qg) */
+    const long qpw = (long)KNN_TQ * (c->i8 ? knn_i8_qg(c->klx, c->lpq, c->n) : 1);
+    const long nqb = (long)((c->nq + qpw - 1) / qpw);
     const long ntiles = (long)((nc + KNN_TC - 1) / KNN_TC);
     /* the re-search of a few uncertified queries: one query block, so the
      * launch's span is one workgroup's scan -- as many splits as the merge

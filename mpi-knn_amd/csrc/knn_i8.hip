@@ -262,7 +262,7 @@ __device__ __forceinline__ int i8_blk_of(const LDS_AS i8_tab_lds *tab, int t)
 // MFMA, survivor counters) were measured with the tuning
 // harness at commit 8ea8e2a; the product source carries no hooks.
 // ---------------------------------------------------------------------------
-template <int KL, int NKS, int W, int WPS, int NST, int NB, int TM>
+template <int KL, int NKS, int W, int WPS, int NST, int NB, int TM, int QG = 1>
 __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     const signed char *__restrict__ qsh, size_t q_rows_pad, size_t q_base, int nq,
     const knn_i8_blocks_t cb, size_t c_rows_pad, int rs,
@@ -272,7 +272,11 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
 {
     // TM m-blocks (32 rows each) a tile: 4 (128-row tiles) or 2 (64-row
     // half tiles: 4 waves, two workgroups a CU).  The 4 query groups of 32
-    // take RHN = W / 4 waves each, MB = TM / RHN m-blocks a wave.
+    // take RHN = W / 4 waves each, MB = TM / RHN m-blocks a wave.  QG = 2
+    // (short rows, 4 waves): each wave carries two groups of 32 queries
+    // (workgroup queries 32 w.. and 128 + 32 w..) against the same A
+    // fragments and accumulator init words -- every LDS byte read and every
+    // corpus byte staged feeds twice the MFMAs (256 queries a workgroup).
     constexpr int TR = 32 * TM;             // rows a tile
     constexpr int RHN = W / 4;              // waves a query group (row halves)
     constexpr int MB = TM / RHN;            // m-blocks per wave
@@ -283,11 +287,13 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     constexpr int WPW = TR / W;             // norm words a wave stages of each array
     constexpr int NSEG = 8 * WPW;           // a wave's staged piece (both arrays)
     constexpr int NORM0 = NST * CHB;        // norm ring: [NST][W][slot words, init words]
-    constexpr int BUF0 = NORM0 + NST * NRB; // [W][NB][64] survivor d^2, then ids
-    constexpr int XB0 = BUF0 + 2 * W * NB * 256;   // RHN = 2: [8][32] bound exchange (u4, v8, v16)
+    constexpr int BUF0 = NORM0 + NST * NRB; // [W][QG][NB][64] survivor d^2, then ids
+    constexpr int XB0 = BUF0 + 2 * W * QG * NB * 256;   // RHN = 2: [8][32] bound exchange (u4, v8, v16)
     constexpr int TB0 = XB0 + (RHN == 2 ? 3 * 8 * 32 * 4 : 0);   // block table
     static_assert(MB == 2 || MB == 4, "m-blocks a wave");
     static_assert(PW == 2 || PW == 4, "DMA pieces a wave");
+    static_assert(QG == 1 || (QG == 2 && RHN == 1 && NKS <= 8), "two query groups: 4-wave short-row kernels");
+    constexpr int QB = 128 * QG;            // queries a workgroup
     constexpr int LDSB = TB0 + (int)((sizeof(i8_tab_lds) + 15) / 16 * 16);
     __shared__ __attribute__((aligned(16))) char smem[LDSB];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -304,9 +310,17 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     const int tb = ntiles / nsplit, tr = ntiles - tb * nsplit;
     const int t_lo = split * tb + (split < tr ? split : tr);
     const int t_hi = t_lo + tb + (split < tr ? 1 : 0);
-    const int qrow0 = qb * 128;
-    const int myq = qrow0 + 32 * qg + r32;
-    const long gq = (long)q_base + myq;
+    const int qrow0 = qb * QB;
+    // query of group g; padding queries (>= nq) load row nq - 1 (with QG = 2
+    // the last block may reach past the query block's rows) and reject all
+    int myq[QG], lq[QG];
+    long gq[QG];
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+        myq[g] = qrow0 + 128 * g + 32 * qg + r32;
+        lq[g] = myq[g] < nq ? myq[g] : nq - 1;
+        gq[g] = (long)q_base + myq[g];
+    }
     constexpr int NCH = (NKS + 3) / 4;      // chunks a tile
     const int nch = NCH;
     const int *qnorms = (const int *)(qsh + q_rows_pad * (size_t)rs);
@@ -314,46 +328,59 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // ---- resident query fragments (B), one per K-step --------------------
     // NKS >= nks K-steps (the instantiation's bucket): those past nks get
     // zero fragments, so the (garbage) corpus bytes they meet add nothing.
-    knn_v4i qf[NKS];
-    {
-        const signed char *qrow = qsh + (size_t)myq * rs + 16 * h;
+    knn_v4i qf[QG][NKS];
+    int qn[QG];   // |q'|^2
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+        const signed char *qrow = qsh + (size_t)lq[g] * rs + 16 * h;
 #pragma unroll
         for (int s = 0; s < NKS; s++) {
             const int sl = s < nks ? s : nks - 1;
             const knn_v4i v = *(const knn_v4i *)(qrow + 32 * sl);
-            qf[s] = s < nks ? v : (knn_v4i){0, 0, 0, 0};
+            qf[g][s] = s < nks ? v : (knn_v4i){0, 0, 0, 0};
         }
+        qn[g] = i8_norm_of(qnorms[i8_norm_pos(lq[g])], qnorms[q_rows_pad + i8_norm_pos(lq[g])]);
     }
-    const int qn = i8_norm_of(qnorms[i8_norm_pos(myq)], qnorms[q_rows_pad + i8_norm_pos(myq)]);   // |q'|^2
     // shared per-query bound across splits and ring steps (qthr: bits of a
     // non-negative double, atomicMin).  INT-mode bounds are integers, or the
     // next double above one (strict publication), so floor() is the int bound.
-    int thr = I8_INF;
-    if (qthr != nullptr && myq < nq) {
-        const double td = __longlong_as_double((long long)atomicMin(qthr + myq, 0x7ff0000000000000ull));
-        thr = td >= 2147483647.0 ? I8_INF : (int)td;
+    int thr[QG];
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+        thr[g] = I8_INF;
+        if (qthr != nullptr && myq[g] < nq) {
+            const double td = __longlong_as_double((long long)atomicMin(qthr + myq[g], 0x7ff0000000000000ull));
+            thr[g] = td >= 2147483647.0 ? I8_INF : (int)td;
+        }
     }
     // padding queries of the last block (myq >= nq) reject every candidate:
     // with an open bound their lanes took the insertion path for every row,
     // and the one workgroup holding them set the launch's span (a 7500-row
     // ring step: 134 us against a 74 us average workgroup)
-    if (myq >= nq) thr = -1;
+#pragma unroll
+    for (int g = 0; g < QG; g++)
+        if (myq[g] >= nq) thr[g] = -1;
     // vmcnt(0) through the builtin: hipcc's wait pass then knows the query
     // loads are complete (an asm wait would leave it inserting vmcnt(N)
     // before each later use of qf, draining the LDS-DMA ring)
     __builtin_amdgcn_s_waitcnt(0x0F70);
 
-    int L[KL], I[KL];
+    int L[QG][KL], I[QG][KL];
 #pragma unroll
-    for (int e = 0; e < KL; e++) { L[e] = I8_INF; I[e] = -1; }
+    for (int g = 0; g < QG; g++)
+#pragma unroll
+        for (int e = 0; e < KL; e++) { L[g][e] = I8_INF; I[g][e] = -1; }
     // uj: list slot of the 2-lane bound (low byte) and of the 4-lane bound
     // (W = 8: the query's lanes in both waves; second byte)
     const int ujm = (uj & 255) < KL - 1 ? (uj & 255) : KL - 1;
     const int uj4 = ((uj >> 8) & 255) < KL - 1 ? ((uj >> 8) & 255) : KL - 1;
     LDS_AS int *xb = (LDS_AS int *)(smem + XB0);   // [3][8 waves][32]: u4, v8, v16
-    LDS_AS int *bk = (LDS_AS int *)(smem + BUF0) + wave_s * NB * 64 + lane;   // entry e at bk[64 e]
-    LDS_AS int *bi = bk + W * NB * 64;
-    int cnt = 0;   // buffered survivors of this lane
+    // group g's entry e at bk0[64 (g NB + e)], its id W QG NB 64 words on
+    LDS_AS int *bk0 = (LDS_AS int *)(smem + BUF0) + wave_s * QG * NB * 64 + lane;
+    LDS_AS int *bi0 = bk0 + W * QG * NB * 64;
+    int cnt[QG];   // buffered survivors of this lane
+#pragma unroll
+    for (int g = 0; g < QG; g++) cnt[g] = 0;
     LDS_AS i8_tab_lds *tab = (LDS_AS i8_tab_lds *)(smem + TB0);
     if (threadIdx.x == 0) {
 #pragma unroll
@@ -399,7 +426,10 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         const unsigned dst = lds0 + ((unsigned)s_x % NST) * (unsigned)CHB + (unsigned)wave_s * (unsigned)(CHB / W);
         if constexpr (PW == 4) bglds16x4(i8_rsrc(s_row + s_coff), voff[0], voff[1], voff[2], voff[3], dst);
         else bglds16x2(i8_rsrc(s_row + s_coff), voff[0], voff[1], dst);
-        if (s_x < total && s_coff == 0) {
+        // (one-chunk tiles: every stage carries its norm piece, the tail's
+        // re-stages too -- the last tile's words again -- so that wait_next
+        // can count it)
+        if ((NCH == 1 || s_x < total) && s_coff == 0) {
             // the tile's two norm arrays in one piece a wave: lanes <
             // WPW / 4 the slot words, the next WPW / 4 lanes the init words
             // of the same rows (c_rows_pad words further on)
@@ -426,9 +456,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         }
     };
     // the next chunk's own pieces landed: the NST - 3 chunks staged after it
-    // may stay in flight
+    // may stay in flight.  One-chunk tiles (SIFT) count each stage's norm
+    // piece too: counted as PW a stage, the wait also drained a third of the
+    // younger stages and the ring ran ~2 tiles ahead instead of NST - 3.
+    // (The shared-bound loads issued between stages only make it stricter.)
     auto wait_next = [&]() {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (NST - 3)) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NCH == 1 ? PW + 1 : PW) * (NST - 3)) : "memory");
     };
     // A fragments (MB m-blocks) of K-step ks of staged chunk xx
     // norm ring: byte offset of 16-byte group v (i8_norm_pos order, 4 words)
@@ -478,23 +511,26 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // 12-entry lists; a query's LPQ lanes hold 8 / 16 rows at or below
     // their L[S8] / L[S16])
     constexpr bool REREAD = KL != KNN_I8_KL_L;
-    constexpr bool SUM = REREAD && KL == KNN_I8_KL_S;
+    // (QG = 2: no summaries -- their 8 VGPRs a group spill there)
+    constexpr bool SUM = REREAD && KL == KNN_I8_KL_S && QG == 1;
     constexpr int S8 = 8 / LPQ - 1, S16 = 16 / LPQ - 1;
-    int q_pubx = -1000;
-    auto qsum_publish = [&](int v8, int v16) {
-        if (!SUM || qsum == nullptr || rh != 0 || h != 0 || myq >= nq) return;
-        if (v8 >= I8_INF || s_x - q_pubx < 4 * nch) return;
-        q_pubx = s_x;
+    int q_pubx[QG];
+#pragma unroll
+    for (int g = 0; g < QG; g++) q_pubx[g] = -1000;
+    auto qsum_publish = [&](int g, int v8, int v16) {
+        if (!SUM || qsum == nullptr || rh != 0 || h != 0 || myq[g] >= nq) return;
+        if (v8 >= I8_INF || s_x - q_pubx[g] < 4 * nch) return;
+        q_pubx[g] = s_x;
         const unsigned long long val = ((unsigned long long)(unsigned)v8 << 32) | (unsigned)v16;
-        unsigned long long *pq = qsum + (size_t)myq * 4 + (split & 3);
+        unsigned long long *pq = qsum + (size_t)myq[g] * 4 + (split & 3);
         asm volatile("global_atomic_umin_x2 %0, %1, off" ::"v"(pq), "v"(val) : "memory");
     };
-    auto refresh = [&]() {
-        int lmin = L[KL - 1], u = L[0], u4 = L[0];
+    auto refresh = [&](int g) {
+        int lmin = L[g][KL - 1], u = L[g][0], u4 = L[g][0];
 #pragma unroll
         for (int e = 1; e < KL; e++) {
-            u = (e == ujm) ? L[e] : u;
-            u4 = (e == uj4) ? L[e] : u4;
+            u = (e == ujm) ? L[g][e] : u;
+            u4 = (e == uj4) ? L[g][e] : u4;
         }
         const int lo = __shfl_xor(lmin, 32), uo = __shfl_xor(u, 32), u4o = __shfl_xor(u4, 32);
         lmin = lo < lmin ? lo : lmin;
@@ -515,7 +551,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             // the split's summary for the other splits: v8 / v16 = the max
             // over the query's LPQ lanes of L[S8] / L[S16] -- 8 / 16 rows of
             // this split lie at or below them
-            int v8 = L[S8], v16 = L[S16];
+            int v8 = L[g][S8], v16 = L[g][S16];
             const int v8o = __shfl_xor(v8, 32), v16o = __shfl_xor(v16, 32);
             v8 = v8o > v8 ? v8o : v8;
             v16 = v16o > v16 ? v16o : v16;
@@ -528,25 +564,26 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 v8 = p8 > v8 ? p8 : v8;
                 v16 = p16 > v16 ? p16 : v16;
             }
-            qsum_publish(v8, v16);
+            qsum_publish(g, v8, v16);
         }
-        thr = nb < thr ? nb : thr;
+        thr[g] = nb < thr[g] ? nb : thr[g];
     };
     // buffered survivors -> lists, in buffer (= row) order, one entry a
     // round; the rounds are dense: a merge runs when some lane's buffer is
     // full, so most lanes insert a real entry every round
-    auto merge = [&]() {
-        for (int e = 0; __ballot(e < cnt) != 0ull; e++) {
+    auto merge = [&](int g) {
+        const LDS_AS int *bk = bk0 + g * NB * 64, *bi = bi0 + g * NB * 64;
+        for (int e = 0; __ballot(e < cnt[g]) != 0ull; e++) {
             int d = I8_INF, id = -1;
-            if (e < cnt) {
+            if (e < cnt[g]) {
                 d = bk[64 * e];
                 id = bi[64 * e];
                 d = d > 0 ? d : I8_INF;   // d^2 == 0: an exact duplicate (serial:86)
             }
-            i8_insert<KL>(L, I, d, id);
+            i8_insert<KL>(L[g], I[g], d, id);
         }
-        cnt = 0;
-        refresh();
+        cnt[g] = 0;
+        refresh(g);
     };
     // The shared bound may fall while the workgroup runs (other splits end,
     // and the merge of an earlier ring step publishes the running answer
@@ -561,36 +598,49 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // load issued with s_x = X0 stages out is older than stage X0's pieces;
     // at an epilogue with xdone > X0 the wait before barrier B(xdone) (or,
     // on the last tile, B(total - 1) >= X0) has seen stage X0 land.
-    unsigned long long q_bits = 0x7ff0000000000000ull;
-    knn_v4i qs0 = {I8_INF, I8_INF, I8_INF, I8_INF}, qs1 = qs0;   // qsum slots 0-1, 2-3
+    unsigned long long q_bits[QG];
+    knn_v4i qs0[QG], qs1[QG];   // qsum slots 0-1, 2-3
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+        q_bits[g] = 0x7ff0000000000000ull;
+        qs0[g] = (knn_v4i){I8_INF, I8_INF, I8_INF, I8_INF};
+        qs1[g] = qs0[g];
+    }
     int q_ready = -1;   // -1: no load pending
     auto qthr_issue = [&](int xnow) {
-        const unsigned long long *pq = qthr + myq;
-        asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(q_bits) : "v"(pq) : "memory");
-        if (SUM && qsum != nullptr) {
-            const unsigned long long *ps = qsum + (size_t)myq * 4;
-            asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(qs0) : "v"(ps) : "memory");
-            asm volatile("global_load_dwordx4 %0, %1, off offset:16 sc1" : "=v"(qs1) : "v"(ps) : "memory");
+#pragma unroll
+        for (int g = 0; g < QG; g++) {
+            const unsigned long long *pq = qthr + lq[g];
+            asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(q_bits[g]) : "v"(pq) : "memory");
+            if (SUM && qsum != nullptr) {
+                const unsigned long long *ps = qsum + (size_t)lq[g] * 4;
+                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(qs0[g]) : "v"(ps) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:16 sc1" : "=v"(qs1[g]) : "v"(ps) : "memory");
+            }
         }
         q_ready = xnow;
     };
     auto qthr_apply = [&]() {
-        asm volatile("" : "+v"(q_bits));
-        if constexpr (SUM) asm volatile("" : "+v"(qs0), "+v"(qs1));
-        const double td = __longlong_as_double((long long)q_bits);
-        int tq = td >= 2147483647.0 ? I8_INF : (int)td;
-        if (SUM && qsum != nullptr) {
-            // slot s = (v16, v8) as (lo, hi) dwords: qs0 = {v16_0, v8_0, v16_1, v8_1}
-            const int a8 = qs0.y > qs0.w ? qs0.y : qs0.w, b8 = qs1.y > qs1.w ? qs1.y : qs1.w;
-            const int b4 = a8 > b8 ? a8 : b8;                        // 4 splits x 8 rows
-            const int s1 = qs0.x < qs0.z ? qs0.x : qs0.z, l1 = qs0.x < qs0.z ? qs0.z : qs0.x;
-            const int s2 = qs1.x < qs1.z ? qs1.x : qs1.z, l2 = qs1.x < qs1.z ? qs1.z : qs1.x;
-            const int m1 = s1 > s2 ? s1 : s2, m2 = l1 < l2 ? l1 : l2;
-            const int b2 = m1 < m2 ? m1 : m2;                        // 2nd smallest v16: 2 x 16 rows
-            const int bs = b4 < b2 ? b4 : b2;
-            tq = bs < tq ? bs : tq;
+#pragma unroll
+        for (int g = 0; g < QG; g++) {
+            asm volatile("" : "+v"(q_bits[g]));
+            if constexpr (SUM) asm volatile("" : "+v"(qs0[g]), "+v"(qs1[g]));
+            const double td = __longlong_as_double((long long)q_bits[g]);
+            int tq = td >= 2147483647.0 ? I8_INF : (int)td;
+            if (SUM && qsum != nullptr) {
+                // slot s = (v16, v8) as (lo, hi) dwords: qs0 = {v16_0, v8_0, v16_1, v8_1}
+                const knn_v4i x0 = qs0[g], x1 = qs1[g];
+                const int a8 = x0.y > x0.w ? x0.y : x0.w, b8 = x1.y > x1.w ? x1.y : x1.w;
+                const int b4 = a8 > b8 ? a8 : b8;                        // 4 splits x 8 rows
+                const int s1 = x0.x < x0.z ? x0.x : x0.z, l1 = x0.x < x0.z ? x0.z : x0.x;
+                const int s2 = x1.x < x1.z ? x1.x : x1.z, l2 = x1.x < x1.z ? x1.z : x1.x;
+                const int m1 = s1 > s2 ? s1 : s2, m2 = l1 < l2 ? l1 : l2;
+                const int b2 = m1 < m2 ? m1 : m2;                        // 2nd smallest v16: 2 x 16 rows
+                const int bs = b4 < b2 ? b4 : b2;
+                tq = bs < tq ? bs : tq;
+            }
+            thr[g] = tq < thr[g] ? tq : thr[g];
         }
-        thr = tq < thr ? tq : thr;
         q_ready = -1;
     };
 
@@ -610,23 +660,25 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // above every d^2 (n 255^2 < DMAX); masked slots take acc = INT_MIN /
     // v = vnone = T_open - 1, below every threshold.
     const int dmax = rs * 65025 + 1;
-    const int t_open = 32 * (qn - dmax), vnone = t_open - 1;
+    int vnone[QG];
+#pragma unroll
+    for (int g = 0; g < QG; g++) vnone[g] = 32 * (qn[g] - dmax) - 1;
     constexpr int A_NONE = (int)0x80000000;
-    auto thr_v = [&]() -> int {
-        const int lim = L[KL - 1] < thr ? L[KL - 1] : thr;
-        return lim >= dmax ? t_open : 32 * (qn - lim);
+    auto thr_v = [&](int g) -> int {
+        const int lim = L[g][KL - 1] < thr[g] ? L[g][KL - 1] : thr[g];
+        return lim >= dmax ? vnone[g] + 1 : 32 * (qn[g] - lim);
     };
-    auto thr_a = [&]() -> int {
-        const int lim = L[KL - 1] < thr ? L[KL - 1] : thr;
-        return lim >= dmax ? A_NONE + 1 : (qn - lim + 1) >> 1;
+    auto thr_a = [&](int g) -> int {
+        const int lim = L[g][KL - 1] < thr[g] ? L[g][KL - 1] : thr[g];
+        return lim >= dmax ? A_NONE + 1 : (qn[g] - lim + 1) >> 1;
     };
     constexpr bool ACCF = NKS <= 8;
-    auto epilogue = [&](int t, knn_v16i (&A)[MB], int xdone) {
+    auto epilogue = [&](int t, knn_v16i (&A)[QG][MB], int xdone) {
         const int lt = t - e_t0;
         const LDS_AS char *cn = (const LDS_AS char *)smem + NORM0 + ((unsigned)t % NST) * NRB;
         const int row0 = lt * TR + 32 * MB * rh;
-        const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 32 * qg;
-        const bool masked = (row0 + 32 * MB > nc) || (gw0 < gt0 + 32 * MB && gt0 < gw0 + 32);
+        const long gt0 = (long)c_base + row0;
+        const bool rmask = row0 + 32 * MB > nc;
         const int idb = (int)(c_base + row0) + 4 * h;
         if constexpr (REREAD) {
             if (qthr != nullptr) {
@@ -634,20 +686,25 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 if (q_ready < 0 && (NCH == 1 || (t & 1) == 0)) qthr_issue(s_x);   // mnist: 3.89 -> 3.84 ms (kbench8)
             }
         }
-        // groups of 2 m-blocks = 32 candidates a lane, lower rows first (the
-        // stable tie order across groups; inside one, v orders by row)
 #pragma unroll
-        for (int g = 0; g < MB / 2; g++) {
+        for (int g = 0; g < QG; g++) {
+        const long gw0 = (long)q_base + qrow0 + 128 * g + 32 * qg;
+        const bool masked = rmask || (gw0 < gt0 + 32 * MB && gt0 < gw0 + 32);
+        LDS_AS int *bk = bk0 + g * NB * 64, *bi = bi0 + g * NB * 64;
+        // pairs of m-blocks = 32 candidates a lane, lower rows first (the
+        // stable tie order across pairs; inside one, v orders by row)
+#pragma unroll
+        for (int pr = 0; pr < MB / 2; pr++) {
             int a[32];
 #pragma unroll
             for (int bb = 0; bb < 2; bb++)
 #pragma unroll
-                for (int i = 0; i < 16; i++) a[16 * bb + i] = A[2 * g + bb][i];
+                for (int i = 0; i < 16; i++) a[16 * bb + i] = A[g][2 * pr + bb][i];
             if (masked) {   // rows past the block, and the query itself (acc > -2^25 otherwise)
 #pragma unroll
                 for (int x = 0; x < 32; x++) {
-                    const int rloc = 32 * (2 * g + (x >> 4)) + 8 * ((x >> 2) & 3) + (x & 3);
-                    if (!(row0 + rloc + 4 * h < nc && idb + rloc != gq)) a[x] = A_NONE;
+                    const int rloc = 32 * (2 * pr + (x >> 4)) + 8 * ((x >> 2) & 3) + (x & 3);
+                    if (!(row0 + rloc + 4 * h < nc && idb + rloc != gq[g])) a[x] = A_NONE;
                 }
             }
             // short rows (NKS <= 8: SIFT) -- most groups end here, late in
@@ -655,7 +712,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             // some lane of the wave (kbench8 counters), so the exact keys
             // are built straight away
             if constexpr (ACCF) {
-                if (__ballot(i8_max32(a) >= thr_a()) == 0ull) continue;
+                if (__ballot(i8_max32(a) >= thr_a(g)) == 0ull) continue;
             }
             // exact keys of the group (slot words from the norm ring)
             int v[32];
@@ -663,15 +720,15 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             for (int bb = 0; bb < 2; bb++)
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const knn_v4i c4 = *(const LDS_AS knn_v4i *)(cn + nofs(4 * h + 8 * (MB * rh + 2 * g + bb) + j));
+                    const knn_v4i c4 = *(const LDS_AS knn_v4i *)(cn + nofs(4 * h + 8 * (MB * rh + 2 * pr + bb) + j));
 #pragma unroll
                     for (int i = 0; i < 4; i++) v[16 * bb + 4 * j + i] = (int)((unsigned)a[16 * bb + 4 * j + i] * 64u + (unsigned)c4[i]);
                 }
             if (masked) {
 #pragma unroll
-                for (int x = 0; x < 32; x++) v[x] = a[x] == A_NONE ? vnone : v[x];
+                for (int x = 0; x < 32; x++) v[x] = a[x] == A_NONE ? vnone[g] : v[x];
             }
-            int T = thr_v();
+            int T = thr_v(g);
             int vm = i8_max32(v);
             if (__ballot(vm >= T) == 0ull) continue;
             // survivors in (d^2, row) order, one a round per lane: into the
@@ -680,16 +737,17 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             do {
                 if (vm >= T) {
                     const int slot = 31 - (vm & 31);
-                    bk[64 * cnt] = qn - (vm >> 5);   // d^2 (0 = a duplicate: dropped at the merge)
-                    bi[64 * cnt] = idb + 32 * (2 * g + (slot >> 4)) + 8 * ((slot >> 2) & 3) + (slot & 3);
-                    cnt++;
+                    bk[64 * cnt[g]] = qn[g] - (vm >> 5);   // d^2 (0 = a duplicate: dropped at the merge)
+                    bi[64 * cnt[g]] = idb + 32 * (2 * pr + (slot >> 4)) + 8 * ((slot >> 2) & 3) + (slot & 3);
+                    cnt[g]++;
                 }
-                if (__ballot(cnt == NB) != 0ull) {
-                    merge();
-                    T = thr_v();
+                if (__ballot(cnt[g] == NB) != 0ull) {
+                    merge(g);
+                    T = thr_v(g);
                 }
-                vm = i8_next(v, vm, vnone);
+                vm = i8_next(v, vm, vnone[g]);
             } while (__ballot(vm >= T) != 0ull);
+        }
         }
     };
 
@@ -720,8 +778,8 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             // tile's start, straight into the accumulator registers: held
             // from earlier they cost 32 more VGPRs, or 16 v_mov_b64 a tile
             // where the next tile's set is loaded beside the live one)
-            knn_v16i acc[MB];
-            rdI(t, acc);
+            knn_v16i acc[QG][MB];
+            rdI(t, acc[0]);
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 const int kt = NKS - 4 * c < 4 ? NKS - 4 * c : 4;   // static after unrolling
@@ -744,9 +802,16 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                             // MFMAs and the epilogue
                             stage();
                         }
+                        // (QG = 2: the first K-step of group 1 takes
+                        // group 0's init words as its C operand)
 #pragma unroll
-                        for (int bb = 0; bb < MB; bb++)
-                            acc[bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(acur[bb], qf[4 * c + ks], acc[bb], 0, 0, 0);
+                        for (int bb = 0; bb < MB; bb++) {
+                            const knn_v16i c0 = acc[0][bb];
+#pragma unroll
+                            for (int g = 0; g < QG; g++)
+                                acc[g][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                                    acur[bb], qf[g][4 * c + ks], (c == 0 && ks == 0) ? c0 : acc[g][bb], 0, 0, 0);
+                        }
 #pragma unroll
                         for (int bb = 0; bb < MB; bb++) acur[bb] = anxt[bb];
                     }
@@ -760,19 +825,22 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             if (q_ready >= 0) qthr_apply();
         }
     }
-    merge();
+#pragma unroll
+    for (int g = 0; g < QG; g++) merge(g);
 
     // strict publication (INT mode, exact keys): if neither lane's list ends
     // at thr, nothing equal to thr was turned away, so every rejected
     // candidate has d^2 >= next(thr) (k_finalize certifies tau < T); W = 8:
     // T of the query = min over its two waves (LDS, after a barrier)
-    int lastmin = L[KL - 1];
+#pragma unroll
+    for (int g = 0; g < QG; g++) {
+    int lastmin = L[g][KL - 1];
     {
         const int o = __shfl_xor(lastmin, 32);
         lastmin = o < lastmin ? o : lastmin;
     }
-    double pub = thr == I8_INF ? KNN_INF : (double)thr;
-    if (lastmin > thr && thr < I8_INF) pub = nextafter((double)thr, KNN_INF);
+    double pub = thr[g] == I8_INF ? KNN_INF : (double)thr[g];
+    if (lastmin > thr[g] && thr[g] < I8_INF) pub = nextafter((double)thr[g], KNN_INF);
     if constexpr (RHN == 2) {
         double *xd = (double *)((char *)smem + NORM0);   // the norm ring is free now
         __syncthreads();
@@ -783,16 +851,17 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             pub = po < pub ? po : pub;
         }
     }
-    if (myq < nq) {
-        const size_t base = (((size_t)split * nq_pad + myq) * LPQ + 2 * rh + h) * KL;
+    if (myq[g] < nq) {
+        const size_t base = (((size_t)split * nq_pad + myq[g]) * LPQ + 2 * rh + h) * KL;
 #pragma unroll
         for (int e = 0; e < KL; e++) {
-            part_d[base + e] = L[e] == I8_INF ? KNN_INF : (double)L[e];
-            part_i[base + e] = I[e];
+            part_d[base + e] = L[g][e] == I8_INF ? KNN_INF : (double)L[g][e];
+            part_i[base + e] = I[g][e];
         }
-        if (h == 0 && rh == 0) part_T[(size_t)split * nq_pad + myq] = pub;
-        if (h == 0 && qthr != nullptr && thr < I8_INF)
-            atomicMin(qthr + myq, (unsigned long long)__double_as_longlong((double)thr));
+        if (h == 0 && rh == 0) part_T[(size_t)split * nq_pad + myq[g]] = pub;
+        if (h == 0 && qthr != nullptr && thr[g] < I8_INF)
+            atomicMin(qthr + myq[g], (unsigned long long)__double_as_longlong((double)thr[g]));
+    }
     }
 }
 
@@ -898,13 +967,13 @@ extern "C" int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t 
     return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
 }
 
-template <int KL, int NKS, int W, int WPS, int NST, int NB, int TM>
+template <int KL, int NKS, int W, int WPS, int NST, int NB, int TM, int QG = 1>
 static void launch_i8(dim3 grid, hipStream_t s, const void *qsh, size_t q_rows_pad, size_t q_base,
                       int nq, const knn_i8_blocks_t &cb, size_t c_rows_pad, int rs,
                       int nks, int ntiles, int nsplit, int nqb, double *part_d, int *part_i,
                       double *part_T, int nq_pad, double *qthr, int uj, unsigned long long *qsum)
 {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KL, NKS, W, WPS, NST, NB, TM>), grid, dim3(64 * W), 0, s,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk_i8<KL, NKS, W, WPS, NST, NB, TM, QG>), grid, dim3(64 * W), 0, s,
                        (const signed char *)qsh, q_rows_pad, q_base, nq, cb, c_rows_pad, rs, nks, ntiles,
                        nsplit, nqb, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj,
                        KL != KNN_I8_KL_L ? qsum : nullptr);
@@ -916,7 +985,8 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int lpq, int k, const void *qs
                                   int nq_pad, double *qthr, unsigned long long *qsum, void *stream)
 {
     const int rs = (int)knn_s8_rs((size_t)n), nks = rs / 32;
-    const int nqb = (nq + 127) / 128;
+    const int qg = knn_i8_qg(kl, lpq, (size_t)n);
+    const int nqb = (nq + 128 * qg - 1) / (128 * qg);
     if (!cbp || cbp->nblk < 1 || cbp->nblk > KNN_I8_MAXBLK) return KNN_ERR_INVALID;
     // the table the kernel walks: block b = tiles [t0[b], t0[b+1]) of its
     // ceil(nc/128) tiles, ascending bases, rows inside the capacity
@@ -938,7 +1008,9 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int lpq, int k, const void *qs
     }
     const int ntiles = cb.t0[cb.nblk];
     if (nqb <= 0 || nsplit <= 0 || k <= 0 || k > kp || kl <= 0 || nks > 28) return KNN_ERR_INVALID;
-    if ((size_t)nqb * 128 > q_rows_pad || nq_pad < nqb * 128) return KNN_ERR_INVALID;
+    // (QG = 2: the last block's padding queries load row nq - 1 and write nothing)
+    if (qg == 1 && ((size_t)nqb * 128 > q_rows_pad || nq_pad < nqb * 128)) return KNN_ERR_INVALID;
+    if ((size_t)nq > q_rows_pad || nq > nq_pad) return KNN_ERR_INVALID;
     // lane-list slot of the shared bound: the 2 lanes of a query cover k + 1
     int uj = (k + 1 + 1) / 2 - 1, uj4 = (k + 1 + 3) / 4 - 1;
     const int no2 = uj > kl - 1;   // 2 lists of kl cannot hold k + 1
@@ -970,7 +1042,10 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int lpq, int k, const void *qs
         // share a CU -- each SIMD runs one wave of each, whose barriers and
         // epilogues are independent: one's epilogue runs under the other's
         // MFMAs (the 8-wave form's two waves a SIMD sat at the same barriers)
-        if (nks <= 4) launch_i8<KNN_I8_KL_S, 4, 4, 2, 8, 5, 2>(I8_ARGS);
+        // Rows of <= 4 K-steps (SIFT): two query groups a wave, a 7-stage
+        // ring (the second group's survivor buffers take the 8th stage's LDS)
+        if (nks <= 4 && qg == 2) launch_i8<KNN_I8_KL_S, 4, 4, 2, 7, 5, 2, 2>(I8_ARGS);
+        else if (nks <= 4) launch_i8<KNN_I8_KL_S, 4, 4, 2, 8, 5, 2>(I8_ARGS);
         else if (nks <= 8) launch_i8<KNN_I8_KL_S, 8, 4, 2, 8, 5, 2>(I8_ARGS);
         else if (nks <= 16) launch_i8<KNN_I8_KL_S, 16, 4, 2, 8, 5, 2>(I8_ARGS);
         else if (nks <= 25) launch_i8<KNN_I8_KL_S, 25, 4, 2, 8, 5, 2>(I8_ARGS);

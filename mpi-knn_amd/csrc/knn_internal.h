@@ -6,6 +6,7 @@
 #define KNN_INTERNAL_H
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "knn.h"
 
 #ifdef __cplusplus
@@ -106,6 +107,15 @@ static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL_S : KNN_
  * lists on 64-row half tiles (the k <= 32 default); 4 for the 8-wave
  * kernel on 128-row tiles (17-entry lists, or KNN_I8_W8=1) */
 static inline int knn_i8_lpq(int kp, int kl) { return kp <= KNN_KP_M && kl != KNN_I8_KL_S ? 4 : 2; }
+/* query groups a wave of the int8 kernel: 2 for the half-tile kernel on
+ * rows of <= 4 K-steps (SIFT's n = 128: a workgroup of 256 queries, A
+ * fragments and init words shared by both groups), else 1
+ * (KNN_I8_QG1=1 forces 1).  A workgroup covers 128 qg queries. */
+static inline int knn_i8_qg(int kl, int lpq, size_t n)
+{
+    const char *e = getenv("KNN_I8_QG1");
+    return kl == KNN_I8_KL_S && lpq == 2 && knn_s8_rs(n) / 32 <= 4 && !(e && *e && *e != '0') ? 2 : 1;
+}
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
 {
     return knn_round_up(n ? n : 1, 128 / knn_esize(dtype));

@@ -70,13 +70,29 @@ def patch(s, name):
         old = "        else bglds16x2(i8_rsrc(s_row + s_coff), voff[0], voff[1], dst);\n"
         assert old in s
         s = s.replace(old, "        else bglds16(i8_rsrc(s_row + s_coff), voff[0], dst);\n")
-        old = 'asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (NST - 3)) : "memory");'
+        old = 'asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NCH == 1 ? PW + 1 : PW) * (NST - 3)) : "memory");'
         assert old in s
-        s = s.replace(old, 'asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PW / 2) * (NST - 3)) : "memory");')
+        s = s.replace(old, 'asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NCH == 1 ? PW / 2 + 1 : PW / 2) * (NST - 3)) : "memory");')
     if "nowait" in name:
-        old = 'asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (NST - 3)) : "memory");'
+        old = 'asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NCH == 1 ? PW + 1 : PW) * (NST - 3)) : "memory");'
         assert old in s
         s = s.replace(old, '')
+    if "rr4s" in name:   # one-chunk tiles re-read the shared bound every 4th tile
+        old = "(NCH == 1 || (t & 1) == 0)"
+        assert old in s
+        s = s.replace(old, "((t & 3) == 0)")
+    if "nosum" in name:  # no cross-split summaries
+        old = "constexpr bool SUM = REREAD && KL == KNN_I8_KL_S;"
+        assert old in s
+        s = s.replace(old, "constexpr bool SUM = false;")
+    if "norr" in name:   # no shared-bound re-read (nor summaries)
+        old = "constexpr bool REREAD = KL != KNN_I8_KL_L;"
+        assert old in s
+        s = s.replace(old, "constexpr bool REREAD = false;")
+    if "filtonly" in name:   # the init-word filter only, never the keys (timing only)
+        old = "                if (__ballot(i8_max32(a) >= thr_a()) == 0ull) continue;\n"
+        assert old in s
+        s = s.replace(old, old + "                if (a[0] != 0x7fffffff) continue;\n")
     if "nobar" in name:
         old = "                            __builtin_amdgcn_s_barrier();   // B(x + 1)\n"
         assert old in s
