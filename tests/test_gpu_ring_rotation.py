@@ -64,9 +64,11 @@ def loopback_dist(torch, rank, P, packed, metas, wires, engine, schedule="ring")
     def batch_isend_irecv(ops):
         for fn, buf, peer in ops:
             if fn is irecv:
-                # ring: hop h brings the block that started on rank - h - 1;
-                # direct: the receive from a peer brings the peer's own block
-                b = peer if schedule == "direct" else (rank - hop["n"] - 1) % P
+                # ring: hop h brings the block that started on rank - h - 1
+                # (a rotation is P - 1 hops; the rescan pass's second
+                # rotation starts over); direct: the receive from a peer
+                # brings the peer's own block
+                b = peer if schedule == "direct" else (rank - hop["n"] % max(P - 1, 1) - 1) % P
                 forms = {t[b].numel(): t[b] for t in (packed, wires)}
                 if engine.ctx.shadow():
                     sb = shadow(b)

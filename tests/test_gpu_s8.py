@@ -110,12 +110,11 @@ def _dist(torch, g, P, packed, metas, wires, e, schedule, emetas):
 @pytest.mark.parametrize("schedule", ["direct", "ring"])
 @pytest.mark.parametrize("P", [1, 2, 8])
 def test_ring_search_from_s8(knn, oracle, P, schedule, rescan, monkeypatch):
-    """(the loopback models one continuous rotation: the neighbour ring's
-    second rotation for a rescan is covered under gloo, test_ring_cpu.py)"""
+    """(the loopback's hop model restarts its rotation every P - 1 hops, so
+    the neighbour ring's second rotation -- the rescan pass's exchange of
+    element blocks after a byte-block search -- runs here too)"""
     import torch
     import mpiknn.ring as ring
-    if rescan and schedule == "ring" and P > 1:
-        pytest.skip("loopback hop model: one rotation")
     if rescan:
         monkeypatch.setenv("KNN_FORCE_RESCAN", "1")
     X = datasets.mnist_like(2400, 784, seed=9)[0]
