@@ -400,7 +400,7 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     c->block_cap = block_cap;
     c->k = k;
     c->kp = knn_kp_for(k, dtype);
-    c->kl = knn_kl_for(c->kp);
+    c->kl = knn_kl_for(c->kp, dtype);
     c->lpq = 4;
     c->klx = c->kl;
     c->xord = 0;   /* split-major (the XCD-grouped order measured no faster) */

@@ -48,14 +48,21 @@ static inline size_t knn_n_pad(size_t n) { return knn_round_up(n ? n : 1, KNN_BK
 /* state capacity and per-lane list length serving k */
 /* State capacity serving k.  With one corpus split, 16-deep lane lists
  * overflow for P(Bin(32, 1/4) >= 16) * 4 = 0.8% of queries at k = 32 (each
- * a rescan); fp32 has the registers for deeper lists, fp64 (k <= 32) not. */
+ * a rescan); fp32 has the registers for deeper lists, fp64 (k <= 32) not.
+ * fp64 16 < k <= 32 keeps 16-deep lane lists but a 64-entry state: the
+ * GEMM certificate's Td (the smallest value a merge drops) then sits past
+ * the (k + 1)-th candidate's near ties -- with a 32-entry state at k = 30,
+ * 228 of the 60000 real-valued MNIST-shape queries had their 33rd filter
+ * value within 2E of the 30th and took the exact rescan. */
 static inline int knn_kp_for(int k, int dtype)
 {
-    if (dtype != KNN_F32 || k <= 16) return KNN_KP;
+    if (k <= 16) return KNN_KP;
+    if (dtype != KNN_F32) return KNN_KP_M;
     return k <= 32 ? KNN_KP_M : KNN_KP_L;
 }
-static inline int knn_kl_for(int kp)
+static inline int knn_kl_for(int kp, int dtype)
 {
+    if (dtype != KNN_F32) return KNN_KL;
     return kp == KNN_KP ? KNN_KL : kp == KNN_KP_M ? KNN_KL_M : KNN_KL_L;
 }
 /* Corpus chunks of one exact rescan launch (k_rescan_step's grid.y): enough

@@ -1195,6 +1195,21 @@ __global__ __launch_bounds__(256) void k_merge(
     // INT mode with every d^2 below 2^32 ((|q| + |c|)^2 <= 4 max|x|^2 <
     // 2^32; list keys are exact integers, idx >= 0): argmin on packed keys
     const bool small_keys = mode == KNN_MODE_INT && 4.0 * meta[KNN_META_MAXNORM] < 4294967295.0;
+    // GEMM mode: selection stops once the head passes the exact-S window of
+    // the k-th kept entry (dk + 2E, below): such an entry can never reach
+    // the top k, now or after a later merge (d^2_k only falls), so it is
+    // dropped with everything behind it and the head becomes Td, the
+    // smallest dropped value -- a query takes ~k + 1 rounds instead of
+    // KP + 1, and only a query whose near ties crowd the window fills the
+    // state.  dkc = the (k + z)-th selected entry, z = those <= E (d^2 <= E:
+    // possibly S == 0, excluded results), as the window below.
+    const bool gstop = mode == KNN_MODE_GEMM && qblk != nullptr;
+    const double Eq = (gstop && qv) ? knn_cert_E<TE>(n, (double)qblk[qnorm_off + q], meta[KNN_META_MAXNORM],
+                                                     filt, meta[KNN_META_MAXABS])
+                                    : 0.0;
+    int nsel = 0, nzs = 0;
+    double dkc = KNN_INF;
+    bool done = false;
     for (int r = 0; r <= rmax; r++) {
         // segment argmin of the heads by (d^2, idx): DPP row shifts (the
         // minimum of each 16-lane row in its lane 15), row broadcasts into
@@ -1234,7 +1249,12 @@ __global__ __launch_bounds__(256) void k_merge(
                 wi = i1;
             }
         }
-        const bool live = wd != KNN_INF;   // this query still has heads
+        if (gstop && !done && dkc < KNN_INF && wd != KNN_INF &&
+            wd > (dkc + 2.0 * Eq) * (1.0 + 1.0 / 524288.0)) {
+            Td = fmin(Td, wd);   // every later head is >= wd
+            done = true;
+        }
+        const bool live = wd != KNN_INF && !done;   // this query still has heads
         if (__ballot(live) == 0ull) break;
         const unsigned long long wall = __ballot(live && hd == wd && hi == wi);
         const unsigned long long who = wall & segm;
@@ -1251,6 +1271,9 @@ __global__ __launch_bounds__(256) void k_merge(
         if constexpr (PF > 0) wpos += __shfl(opos0, wl);   // state runs: slot in the old state
         if (live) {
             if (r < KP) {
+                nsel++;
+                if (wd <= Eq) nzs++;
+                else if (nsel - nzs == k) dkc = wd;
                 if (sl == r % S) {
 #pragma unroll
                     for (int x = 0; x < NS; x++) {
@@ -2364,10 +2387,12 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
     return hip_status();
 }
 
-// The served (element type, state capacity) pairs: fp64 k <= 32; fp32 k <= 16, 32, 128.
+// The served (element type, state capacity) pairs: fp64 k <= 16, 32 (16-deep
+// lane lists); fp32 k <= 16, 32, 128.
 #define KNN_DISPATCH(dtype, kp, CALL)                                          \
     do {                                                                       \
         if ((dtype) == KNN_F64 && (kp) == KNN_KP) { CALL(double, KNN_KL, KNN_KP); }       \
+        else if ((dtype) == KNN_F64 && (kp) == KNN_KP_M) { CALL(double, KNN_KL, KNN_KP_M); } \
         else if ((dtype) == KNN_F32 && (kp) == KNN_KP) { CALL(float, KNN_KL, KNN_KP); }   \
         else if ((dtype) == KNN_F32 && (kp) == KNN_KP_M) { CALL(float, KNN_KL_M, KNN_KP_M); } \
         else if ((dtype) == KNN_F32 && (kp) == KNN_KP_L) { CALL(float, KNN_KL_L, KNN_KP_L); } \
@@ -2462,6 +2487,8 @@ extern "C" int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const dou
                        (unsigned long long *)qthr, cap, fin, fa)
     if (dtype == KNN_F64 && kp == KNN_KP && kl == KNN_I8_KL_S) RANK(double, KNN_KP, KNN_I8_KL_S);
     else if (dtype == KNN_F64 && kp == KNN_KP) RANK(double, KNN_KP, KNN_I8_KL);
+    else if (dtype == KNN_F64 && kp == KNN_KP_M && kl == KNN_I8_KL_S) RANK(double, KNN_KP_M, KNN_I8_KL_S);
+    else if (dtype == KNN_F64 && kp == KNN_KP_M) RANK(double, KNN_KP_M, KNN_I8_KL);
     else if (dtype == KNN_F32 && kp == KNN_KP && kl == KNN_I8_KL_S) RANK(float, KNN_KP, KNN_I8_KL_S);
     else if (dtype == KNN_F32 && kp == KNN_KP) RANK(float, KNN_KP, KNN_I8_KL);
     else if (dtype == KNN_F32 && kp == KNN_KP_M && kl == KNN_I8_KL_S) RANK(float, KNN_KP_M, KNN_I8_KL_S);

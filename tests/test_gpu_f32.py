@@ -269,3 +269,26 @@ def test_split_filter_fp64_blocks(knn, oracle, monkeypatch, m, n):
     base, _, ub = run_engine(X, 30, dtype="f64")
     assert got.tobytes() == base.tobytes()
     assert u <= ub + max(2, m // 200)
+
+
+def test_gemm_state_holds_near_ties(knn, oracle):
+    """fp64 GEMM mode, k = 30: each of 50 centre rows has 40 rows at one
+    distance (0.5, spread 1e-9 -- inside the certificate window E ~ 1e-3 of
+    one another).  The 64-entry state (knn_kp_for, fp64 16 < k <= 32) keeps
+    all 40, so the smallest value a merge drops (Td) lies past the window
+    and every query is certified in the first pass; a 32-entry state
+    dropped the 33rd inside the window and sent each centre to the exact
+    rescan.  Bit-exact vs the oracle either way."""
+    rng = np.random.default_rng(5)
+    n, nc = 64, 50
+    C = rng.uniform(0, 1, (nc, n))
+    parts = [C]
+    for i in range(nc):
+        u = rng.normal(0, 1, (40, n))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        parts.append(C[i] + 0.5 * u * (1 + 1e-9 * rng.standard_normal((40, 1))))
+    X = np.vstack(parts)
+    got, mode, u = run_engine(X, 30, dtype="f64")
+    assert mode == 1   # GEMM
+    assert_same(got, oracle.knn(X, 30), "near-tie crowd f64")
+    assert u == 0, u
