@@ -832,6 +832,15 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
      * 0.67 ms a rank, the model's 8 */
     if (c->i8 && c->i8_wgpc == 2 && !short_rows && nqb * s_min >= slots) {
         best = s_min;
+        /* between one and two rounds at s_min (a P = 4 rank's launches:
+         * 118 query blocks x 7 splits on 512 slots), one full round wins
+         * when its lane lists stay short enough (<= 6000 rows a list; MNIST
+         * P = 1 left 2 queries uncertified at 5000, 58 at 7500): emulated
+         * P = 4 rank 4 / 5 / 7 / 9 splits 1.121 / 1.233 / 1.187 / 1.193 ms */
+        const long s1 = slots / nqb;
+        if (nqb * s_min < 2L * slots && s1 >= 1 && s1 < s_min &&
+            (double)nc / ((double)s1 * c->lpq) <= 6000.0)
+            best = (int)s1;
         const int e = c->split_next++ % KNN_SPLIT_CACHE;
         c->split_cache[e].nc = nc;
         c->split_cache[e].lpq = c->lpq;
