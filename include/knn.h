@@ -34,6 +34,9 @@
  *   KNN_NO_QSUM=1         int8 kernels without the cross-split summaries
  *   KNN_I8_W8=1           12-entry int8 lists on the 8-wave kernel (128-row
  *                         tiles) instead of the 64-row half-tile kernel
+ *   KNN_I8_QG1=1          one query group a wave on rows of <= 128 bytes
+ *                         (the half-tile kernel otherwise carries two: 256
+ *                         queries a workgroup sharing each staged row)
  *   KNN_NO_RANK_MERGE=1   int8 lists merged by k_merge's argmin rounds
  *                         instead of k_merge_rank
  *   KNN_FORCE_RESCAN=1    send every query through the exact rescan pass
