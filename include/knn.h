@@ -358,15 +358,6 @@ KNN_API int knn_ctx_rescan_end(knn_ctx_t *ctx, knn_neighbour_t *d_out, void *str
 KNN_API int knn_search_packed(knn_ctx_t *ctx, const void *d_block, size_t m,
                       knn_neighbour_t *d_out, void *stream);
 
-/* Scheduling hint: the corpus rows the searches of this context fold in
- * all (the ring's m; 0 = unknown, the default).  A ring rank's launches
- * are short (R = m / P rows a block); knowing m, the split choice can give
- * the whole search one round of equal workgroups -- at P = 8 on MNIST the
- * own block as 1 split beside the received blocks' 7 (472 workgroups on
- * 512 slots) instead of 8 + 8 splits run back to back.  Results do not
- * depend on it. */
-KNN_API int knn_ctx_set_search_rows(knn_ctx_t *ctx, size_t rows);
-
 /* Diagnostics of the last knn_ctx_end: engine mode (0 integer-exact,
  * 1 fp64 GEMM + exact re-rank, 2 exact scan) and the corpus split count. */
 KNN_API int knn_ctx_info(const knn_ctx_t *ctx, int *mode, int *splits);

@@ -111,7 +111,6 @@ struct knn_ctx {
      * with 65-entry lane lists and its buffers */
     double hmeta[KNN_META_DOUBLES];
     int have_hmeta;
-    size_t search_rows;       /* knn_ctx_set_search_rows: corpus rows of a search (0: unknown) */
     int sub_research;         /* this context is such a sub-context: 65-entry lists
                                * over the most splits the merge takes */
     int one_block_q8;         /* the search's only step folded its own query byte block */
@@ -465,16 +464,6 @@ int knn_ctx_contraction_bits(const knn_ctx_t *c)
 }
 
 int knn_ctx_split(const knn_ctx_t *c) { return c ? c->split : 0; }
-
-int knn_ctx_set_search_rows(knn_ctx_t *c, size_t rows)
-{
-    if (!c) return KNN_ERR_INVALID;
-    if (c->search_rows != rows) {
-        c->search_rows = rows;
-        for (int e = 0; e < KNN_SPLIT_CACHE; e++) c->split_cache[e].best = 0;
-    }
-    return KNN_OK;
-}
 
 int knn_ctx_info(const knn_ctx_t *c, int *mode, int *splits)
 {
@@ -841,27 +830,6 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
      * work and a set of cold lists.  A single round (a ring rank's fused
      * launch) still takes the model: P = 8 6 / 7 / 8 splits 0.75 / 0.69 /
      * 0.67 ms a rank, the model's 8 */
-    /* a ring rank's search (knn_ctx_set_search_rows: m corpus rows) whose
-     * every launch is a single round: one round of equal workgroups over
-     * the whole search -- L = m nqb / slots rows a workgroup, nc / L splits
-     * this launch -- when the lane lists stay <= 6000 rows (MNIST P = 8:
-     * the own block 1 split beside the received blocks' 7, 472 workgroups
-     * at once, instead of 8 + 8 splits back to back) */
-    if (c->i8 && c->i8_wgpc == 2 && !short_rows && !c->sub_research && c->search_rows > nc &&
-        nqb * s_min < slots) {
-        const double L = (double)c->search_rows * (double)nqb / (double)slots;
-        long s1 = (long)((double)nc / L);
-        if (s1 < 1) s1 = 1;
-        if (L / c->lpq <= 6000.0 && nqb * (long)((double)c->search_rows / L) <= slots && s1 <= smax) {
-            best = (int)s1;
-            const int e = c->split_next++ % KNN_SPLIT_CACHE;
-            c->split_cache[e].nc = nc;
-            c->split_cache[e].lpq = c->lpq;
-            c->split_cache[e].i8 = c->i8;
-            c->split_cache[e].best = best;
-            return best;
-        }
-    }
     if (c->i8 && c->i8_wgpc == 2 && !short_rows && nqb * s_min >= slots) {
         best = s_min;
         /* between one and two rounds at s_min (a P = 4 rank's launches:

@@ -427,7 +427,6 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
                            hipMemcpyHostToDevice);
         if (he != hipSuccess) { rc = KNN_ERR_HIP; break; }
         rc = knn_ctx_create_dt(&e->ctx, e->dev, e->rows, n, R, k, dtype);
-        if (!rc) rc = knn_ctx_set_search_rows(e->ctx, m);   /* split hint */
     }
     for (int g = 0; g < P && !rc; g++)
         if (hipSetDevice(d[g].dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = KNN_ERR_HIP;

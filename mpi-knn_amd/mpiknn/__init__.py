@@ -47,7 +47,7 @@ API_SYMBOLS = (
     "knn_ctx_shadow", "knn_ctx_step_shadow", "knn_ctx_begin_meta", "knn_ctx_shadow_bytes",
     "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n", "knn_ctx_split", "knn_s8_block_bytes",
     "knn_s8_block_meta_offset", "knn_block_pack_s8", "knn_s8_spec_ok", "knn_ctx_begin_s8",
-    "knn_ctx_attach_qblock", "knn_ctx_set_search_rows",
+    "knn_ctx_attach_qblock",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -108,7 +108,6 @@ def _load():
         "knn_ctx_rescan_end": ([p, p, p], i),
         "knn_search_packed": ([p, p, sz, p, p], i),
         "knn_ctx_info": ([p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], i),
-        "knn_ctx_set_search_rows": ([p, sz], i),
         "knn_ctx_contraction_bits": ([p], i),
         "knn_ctx_split": ([p], i),
         "knn_wire_bytes": ([sz, sz, i], sz),
@@ -408,10 +407,6 @@ class Context:
         _check(lib.knn_ctx_profile(self._h, enable, ctypes.byref(dm), ctypes.byref(mm),
                                    ctypes.byref(n)), "knn_ctx_profile")
         return dm.value, mm.value, n.value
-
-    def set_search_rows(self, rows):
-        """knn_ctx_set_search_rows: the corpus rows a search folds (split hint)."""
-        _check(lib.knn_ctx_set_search_rows(self._h, int(rows)), "knn_ctx_set_search_rows")
 
     def info(self):
         mode, splits = ctypes.c_int(), ctypes.c_int()

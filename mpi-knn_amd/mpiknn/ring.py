@@ -212,10 +212,6 @@ class GpuEngine:
         self.ctx.begin(self.qb.data_ptr(), self.R, q_base, self.meta.data_ptr(), self.stream(),
                        h_meta=h_meta)
 
-    def set_search_rows(self, m):
-        """the corpus rows of the searches (the ring's m): split hint"""
-        self.ctx.set_search_rows(m)
-
     def attach_elements(self):
         """before an exact rescan of a search begun from the byte block"""
         if self.spec:
@@ -294,8 +290,6 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
     if schedule not in ("ring", "direct"):
         raise ValueError("unknown ring schedule %r" % (schedule,))
     R, blocks = partition(m, P)
-    if hasattr(engine, "set_search_rows"):
-        engine.set_search_rows(m)   # split hint (knn_ctx_set_search_rows)
     wire = False
     h_meta = None
     if P > 1:

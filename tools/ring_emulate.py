@@ -71,8 +71,6 @@ def main():
                     help="byte-block steps: one launch per block (the neighbour ring), the own "
                          "block then every other block in one launch (the direct-exchange "
                          "ring's default), or all blocks in one launch (KNN_RING_FUSE=all)")
-    ap.add_argument("--no-hint", action="store_true",
-                    help="no knn_ctx_set_search_rows (the split choice sees one launch at a time)")
     args = ap.parse_args()
 
     import torch
@@ -92,8 +90,6 @@ def main():
             os.environ["KNN_SPLITS"] = str(sp)
         R, blocks = ring.partition(m, P)
         eng = ring.GpuEngine(torch, 0, n, R, blocks[0][1], k, dtype=dt)
-        if not args.no_hint:
-            eng.ctx.set_search_rows(m)   # as ring_search does
         sdt = "f32" if Xd.dtype == torch.float32 else "f64"
         eng.pack(Xd[0:blocks[0][1]], layout_col=False)
         nb = mpiknn.block_bytes(R, n, dt)
