@@ -118,12 +118,22 @@ __device__ __forceinline__ int i8_norm_pos(int r)
 // bytes, |x'| <= 128, d^2 <= n 255^2): |acc| < 2^25, |v| < 2^31, and inside
 // one lane (one query) the values span less than 32 (n 255^2 + 1) < 2^31
 // (i8_next).
-__device__ __forceinline__ int i8_norm_word(int r, int nrm)
+//
+// Rows of more than 4 K-steps (rs > 128 bytes: MNIST) take the whole norm
+// in the slot word and a zero init word:
+//     K(r) = 31 - slot(r) - 32 |x'|^2,   IW(r) = 0,
+// so acc = A, v = 64 A + K is the same key, i8_norm_of the same norm, and
+// their kernels start the accumulators at zero instead of reading the init
+// words (k_dist_topk_i8: SHORT) -- the accumulator filter that needs IW
+// runs on short rows only, and on long rows the 8 init-word ds_read_b128 a
+// tile were LDS traffic for nothing (|v| <= 64 n 128^2 + 32 n 128^2 < 2^31).
+__device__ __forceinline__ bool i8_long_rows(int rs) { return rs > 128; }
+__device__ __forceinline__ int i8_norm_word(int r, int nrm, int rs)
 {
     const int rr = r & 127, b = rr >> 5, w = rr & 31;
     const int slot = 16 * (b & 1) + 4 * (w >> 3) + (w & 3);
-    return 31 - slot - 32 * (nrm & 1);
+    return 31 - slot - 32 * (i8_long_rows(rs) ? nrm : (nrm & 1));
 }
-__device__ __forceinline__ int i8_init_word(int nrm) { return -(nrm >> 1); }
+__device__ __forceinline__ int i8_init_word(int nrm, int rs) { return i8_long_rows(rs) ? 0 : -(nrm >> 1); }
 __device__ __forceinline__ int i8_norm_of(int k2, int iw) { return -2 * iw - (k2 >> 5); }
 #endif

@@ -183,8 +183,8 @@ __global__ __launch_bounds__(256) void k_shadow8(signed char *__restrict__ dst, 
         }
         for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
         if (lane == 0) {
-            norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, s);
-            norms[rows_pad + i8_norm_pos((int)r)] = i8_init_word(s);
+            norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, s, rs);
+            norms[rows_pad + i8_norm_pos((int)r)] = i8_init_word(s, rs);
         }
     }
 }
@@ -294,6 +294,10 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     static_assert(PW == 2 || PW == 4, "DMA pieces a wave");
     static_assert(QG == 1 || (QG == 2 && RHN == 1 && NKS <= 8), "two query groups: 4-wave short-row kernels");
     constexpr int QB = 128 * QG;            // queries a workgroup
+    // rows of <= 4 K-steps carry init words (K2 / IW form); longer rows the
+    // whole norm in the slot word and zero init words (knn_device.h): their
+    // accumulators start at zero, no init-word reads
+    constexpr bool SHORT = NKS <= 4;
     constexpr int LDSB = TB0 + (int)((sizeof(i8_tab_lds) + 15) / 16 * 16);
     __shared__ __attribute__((aligned(16))) char smem[LDSB];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -672,7 +676,9 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         const int lim = L[g][KL - 1] < thr[g] ? L[g][KL - 1] : thr[g];
         return lim >= dmax ? A_NONE + 1 : (qn[g] - lim + 1) >> 1;
     };
-    constexpr bool ACCF = NKS <= 8;
+    // short rows (<= 4 K-steps, SIFT; i8_long_rows): the accumulator
+    // filter; their byte blocks carry the init words it needs
+    constexpr bool ACCF = SHORT;
     auto epilogue = [&](int t, knn_v16i (&A)[QG][MB], int xdone) {
         const int lt = t - e_t0;
         const LDS_AS char *cn = (const LDS_AS char *)smem + NORM0 + ((unsigned)t % NST) * NRB;
@@ -707,7 +713,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                     if (!(row0 + rloc + 4 * h < nc && idb + rloc != gq[g])) a[x] = A_NONE;
                 }
             }
-            // short rows (NKS <= 8: SIFT) -- most groups end here, late in
+            // short rows (SHORT: SIFT) -- most groups end here, late in
             // the scan; long rows (MNIST) almost always hold a survivor in
             // some lane of the wave (kbench8 counters), so the exact keys
             // are built straight away
@@ -779,7 +785,14 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             // from earlier they cost 32 more VGPRs, or 16 v_mov_b64 a tile
             // where the next tile's set is loaded beside the live one)
             knn_v16i acc[QG][MB];
-            rdI(t, acc[0]);
+            if constexpr (SHORT) {
+                rdI(t, acc[0]);
+            } else {
+#pragma unroll
+                for (int bb = 0; bb < MB; bb++)
+#pragma unroll
+                    for (int i = 0; i < 16; i++) acc[0][bb][i] = 0;
+            }
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 const int kt = NKS - 4 * c < 4 ? NKS - 4 * c : 4;   // static after unrolling
@@ -892,8 +905,8 @@ __global__ __launch_bounds__(256) void k_gather8(signed char *__restrict__ dst, 
             *(int *)(dst + r * rs + b) = q >= 0 ? *(const int *)(src + (size_t)q * rs + b) : 0;
         if (lane == 0) {
             const int nrm = q >= 0 ? i8_norm_of(sn[i8_norm_pos(q)], sn[src_rows_pad + i8_norm_pos(q)]) : 0;
-            dn[i8_norm_pos((int)r)] = i8_norm_word((int)r, nrm);
-            dn[dst_rows_pad + i8_norm_pos((int)r)] = i8_init_word(nrm);
+            dn[i8_norm_pos((int)r)] = i8_norm_word((int)r, nrm, rs);
+            dn[dst_rows_pad + i8_norm_pos((int)r)] = i8_init_word(nrm, rs);
         }
     }
 }

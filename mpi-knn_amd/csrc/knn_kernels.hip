@@ -379,8 +379,8 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
     if (ty == 0 && i < rows_pad) {
         const double nr = (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]);
         const unsigned ni = (ipart[0][tx] + ipart[1][tx]) + (ipart[2][tx] + ipart[3][tx]);
-        norms[i8_norm_pos((int)i)] = i8_norm_word((int)i, (int)ni);
-        norms[rows_pad + i8_norm_pos((int)i)] = i8_init_word((int)ni);
+        norms[i8_norm_pos((int)i)] = i8_norm_word((int)i, (int)ni, rs);
+        norms[rows_pad + i8_norm_pos((int)i)] = i8_init_word((int)ni, rs);
         if (nr == nr) mnorm = nr;
         else ma.nonfin = 1.0;
     }
@@ -440,8 +440,8 @@ __global__ __launch_bounds__(256) void k_pack8_row(signed char *__restrict__ dst
             si += (unsigned)__shfl_xor((int)si, off);
         }
         if (lane == 0) {
-            norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, (int)si);
-            norms[rows_pad + i8_norm_pos((int)r)] = i8_init_word((int)si);
+            norms[i8_norm_pos((int)r)] = i8_norm_word((int)r, (int)si, rs);
+            norms[rows_pad + i8_norm_pos((int)r)] = i8_init_word((int)si, rs);
         }
         if (s == s) mnorm = s > mnorm ? s : mnorm;
         else ma.nonfin = 1.0;

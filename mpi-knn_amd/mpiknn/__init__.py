@@ -19,7 +19,8 @@ import weakref
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libknn.so")
+# (KNN_LIB_PATH: another build of the same library, for A/B timing runs)
+LIB_PATH = os.environ.get("KNN_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libknn.so")
 
 # knn_neighbour_t (blk:15-20): {double distance; int32 idx (1-based); int32 label}
 NB_DTYPE = np.dtype([("distance", "<f8"), ("idx", "<i4"), ("label", "<i4")])
