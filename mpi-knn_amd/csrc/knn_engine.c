@@ -121,6 +121,12 @@ struct knn_ctx {
     knn_neighbour_t *sub_out;
     unsigned char *sub_flag;
     int *fail_list2;
+    /* the GEMM-mode merge's query order (knn_order.hip), found once a
+     * search from its first merged lists */
+    int *ord_lab, *ord_keys, *ord_iota, *ord_perm;
+    void *ord_tmp;
+    size_t ord_cap, ord_tmp_bytes;
+    int ord_ready;
     /* kernel timing (knn_ctx_profile): 3 events per step bracket
      * k_dist_topk and k_merge */
     int prof_on, prof_pending, prof_launches;
@@ -297,6 +303,11 @@ static void ctx_free_buffers(knn_ctx_t *c)
     if (c->ev_end) hipEventDestroy(c->ev_end);
     hipFree(c->qthr);
     hipFree(c->qsum);
+    hipFree(c->ord_lab);
+    hipFree(c->ord_keys);
+    hipFree(c->ord_iota);
+    hipFree(c->ord_perm);
+    hipFree(c->ord_tmp);
     hipFree(c->st_d);
     hipFree(c->st_x);
     hipFree(c->st_T);
@@ -583,6 +594,7 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
     c->sscale = 0.f;
     c->have_hmeta = 0;
     c->one_block_q8 = 0;
+    c->ord_ready = 0;
     if (!(no_i8 && no_h16 && no_split)) {
         double hm[KNN_META_DOUBLES];
         if (!h_meta) {
@@ -920,6 +932,47 @@ static int rank_merge_ok(const knn_ctx_t *c, int nsplit_total)
            c->lpq * nsplit_total <= 64 && !env_on("KNN_NO_RANK_MERGE");
 }
 
+/* The GEMM-mode merge reads each window candidate's element row at random
+ * (exact S); past the Infinity Cache (a block of more than 64 MB) it merges
+ * the queries in the order of knn_order.hip, so that near queries -- which
+ * share their candidates -- run together (KNN_ORDER=1 forces it,
+ * KNN_NO_ORDER=1 disables it; results do not depend on it). */
+static int want_order(const knn_ctx_t *c, size_t nc)
+{
+    if (c->i8 || c->h16 || env_on("KNN_NO_ORDER")) return 0;
+    if (env_on("KNN_ORDER")) return 1;
+    const size_t bytes = nc * knn_n_pad_dt(c->n, c->dtype) * knn_esize(c->dtype);
+    return c->nq >= 8192 && bytes > ((size_t)64 << 20);
+}
+
+static int find_order(knn_ctx_t *c, int set, int nsplit)
+{
+    if (c->ord_cap < c->nq_pad) {
+        hipFree(c->ord_lab);
+        hipFree(c->ord_keys);
+        hipFree(c->ord_iota);
+        hipFree(c->ord_perm);
+        hipFree(c->ord_tmp);
+        c->ord_lab = c->ord_keys = c->ord_iota = c->ord_perm = NULL;
+        c->ord_tmp = NULL;
+        c->ord_cap = 0;
+        const size_t b = c->nq_pad * sizeof(int);
+        c->ord_tmp_bytes = knn_order_tmp_bytes((int)c->nq_pad);
+        if (hipMalloc((void **)&c->ord_lab, b) != hipSuccess || hipMalloc((void **)&c->ord_keys, b) != hipSuccess ||
+            hipMalloc((void **)&c->ord_iota, b) != hipSuccess || hipMalloc((void **)&c->ord_perm, b) != hipSuccess ||
+            hipMalloc(&c->ord_tmp, c->ord_tmp_bytes ? c->ord_tmp_bytes : 16) != hipSuccess)
+            return KNN_ERR_NOMEM;
+        c->ord_cap = c->nq_pad;
+    }
+    /* 6 rounds: labels settle to cluster-sized pieces (pointer jumping
+     * halves the distance to the piece's minimum each round) */
+    RCHK(knn_launch_order(c->part_i[set], nsplit, c->lpq, c->klx, (int)c->nq, (int)c->nq_pad,
+                          (long long)c->q_base, 6, c->ord_lab, c->ord_keys, c->ord_iota, c->ord_perm, c->ord_tmp,
+                          c->ord_tmp_bytes, c->ms));
+    c->ord_ready = 1;
+    return KNN_OK;
+}
+
 /* fin_out: the search's last merge -- with the rank merge it finalizes
  * too (records into fin_out, *finalized = 1) */
 static int launch_merge_sets_fin(knn_ctx_t *c, int set, int nsets, int nsplit_total, const void *cblk,
@@ -933,11 +986,17 @@ static int launch_merge_sets_fin(knn_ctx_t *c, int set, int nsets, int nsplit_to
                                    c->st_x, c->st_i, c->st_T, c->qthr, fin_out, c->fail_count, c->fail_list,
                                    c->mode_dev, c->fbound, c->meta, (int)c->n, env_on("KNN_FORCE_RESCAN"), c->ms));
         if (fin_out && finalized) *finalized = 1;
-    } else
+    } else {
+        const int *perm = NULL;
+        if (want_order(c, nc)) {
+            if (!c->ord_ready) RCHK(find_order(c, set, nsplit_total));
+            perm = c->ord_perm;
+        }
         RCHK(knn_launch_merge(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
                               nsplit_total, c->lpq, c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x,
                               c->st_i, c->st_T, c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n,
-                              c->meta, c->qthr, c->split, c->ms));
+                              c->meta, c->qthr, c->split, perm, c->ms));
+    }
     c->merged = 1;
     /* (the search's last merge: nothing waits on its sets -- an event
      * record is one more packet on the queue before the read-back) */

@@ -184,7 +184,13 @@ int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *
                      int first_step,
                      double *st_d, double *st_x, int *st_i, double *st_T, const void *qblk,
                      size_t q_rows_pad, const void *cblk, size_t c_base, int nc, int n,
-                     const double *meta, double *qthr, int filt, void *stream);
+                     const double *meta, double *qthr, int filt, const int *qperm, void *stream);
+/* knn_order.hip: a query order for the GEMM-mode merge (queries grouped by
+ * the clusters their list heads connect) */
+size_t knn_order_tmp_bytes(int nq);
+int knn_launch_order(const int *part_i, int nsplit, int lpq, int kl, int nq, int nq_pad, long long q_base,
+                     int rounds, int *lab, int *keys, int *iota, int *perm, void *tmp, size_t tmp_bytes,
+                     void *stream);
 int knn_launch_finalize(int dtype, int kp, const double *st_d, const double *st_x, const int *st_i,
                         const double *st_T, const void *qblk, size_t q_rows_pad,
                         int nq, int n, int k, const double *meta,

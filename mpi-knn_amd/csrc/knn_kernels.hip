@@ -325,8 +325,10 @@ __device__ __forceinline__ int knn_spec8(T v)
 // col-major source (the .mat layout): a workgroup owns 64 rows and walks the
 // columns in 64 x 64 tiles (each wave reads 64 consecutive rows of a column:
 // 512-byte runs), all 16 loads of a thread's tile in flight before their
-// conversion; bytes go through LDS into 16-byte row stores.  Thread (ty, tx)
-// sums row tx's squares over columns = ty mod 4; four partials a row.
+// conversion, and the next tile's 16 issued before this one is converted
+// (32 in flight); bytes go through LDS into 16-byte row stores.  Thread
+// (ty, tx) sums row tx's squares over columns = ty mod 4; four partials a
+// row.
 template <typename T, typename S>
 __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst, size_t rows, size_t rows_pad,
                                                    int n, int rs, const S *__restrict__ src, size_t ld)
@@ -344,12 +346,18 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
     knn_meta_acc ma;
     double s = 0.0;
     unsigned si = 0u;
+    S v[16];
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+        const int j = ty + 4 * e;
+        v[e] = (live && j < n) ? __builtin_nontemporal_load(xp + (size_t)j * ld) : (S)0;
+    }
     for (int j0 = 0; j0 < rs; j0 += 64) {
-        S v[16];
+        S vn[16];
 #pragma unroll
         for (int e = 0; e < 16; e++) {
-            const int j = j0 + ty + 4 * e;
-            v[e] = (live && j < n) ? __builtin_nontemporal_load(xp + (size_t)j * ld) : (S)0;
+            const int j = j0 + 64 + ty + 4 * e;
+            vn[e] = (live && j < n) ? __builtin_nontemporal_load(xp + (size_t)j * ld) : (S)0;
         }
 #pragma unroll
         for (int e = 0; e < 16; e++) {
@@ -371,6 +379,8 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
             *(knn_v4i *)(dst + (i0 + r) * (size_t)rs + j0 + c0) = (knn_v4i){(int)w4[0], (int)w4[1], (int)w4[2], (int)w4[3]};
         }
         __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 16; e++) v[e] = vn[e];
     }
     part[ty][tx] = s;
     ipart[ty][tx] = si;
@@ -1109,7 +1119,8 @@ __global__ __launch_bounds__(256) void k_merge(
     double *__restrict__ st_d, double *__restrict__ st_x, int *__restrict__ st_i,
     double *__restrict__ st_T, const TE *__restrict__ qblk, size_t qnorm_off,
     const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
-    const double *__restrict__ meta, int k, unsigned long long *__restrict__ qthr, int filt)
+    const double *__restrict__ meta, int k, unsigned long long *__restrict__ qthr, int filt,
+    const int *__restrict__ qperm)
 {
     // S lanes a query (64, or 32 when nl + 1 <= 32: two queries a wave, so
     // twice the independent argmin chains a SIMD interleaves -- the merge is
@@ -1119,8 +1130,10 @@ __global__ __launch_bounds__(256) void k_merge(
     const int seg = lane / S, sl = lane - seg * S;
     const int q0 = (blockIdx.x * 4 + wave) * QPW;
     if (q0 >= nq) return;
-    const int q = q0 + seg;
-    const bool qv = q < nq;
+    // qperm (knn_order.hip): the wave's queries in a cache-friendly order
+    const int qi = q0 + seg;
+    const bool qv = qi < nq;
+    const int q = (qperm != nullptr && qv) ? qperm[qi] : qi;
     const unsigned long long segm = (S == 64) ? ~0ull : (0xffffffffull << (32 * seg));
     const int mode = knn_mode<TE>(meta, n);
     const int nl = lpq * nsplit;   // partial lists: [split][query][lpq][kl]
@@ -2420,7 +2433,7 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
                                 int first_step, double *st_d, double *st_x, int *st_i,
                                 double *st_T, const void *qblk, size_t q_rows_pad,
                                 const void *cblk, size_t c_base, int nc, int n,
-                                const double *meta, double *qthr, int filt, void *stream)
+                                const double *meta, double *qthr, int filt, const int *qperm, void *stream)
 {
     if (lpq < 1 || kl < 1 || lpq * nsplit + 1 > 64 || k <= 0 || k > kp) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
@@ -2436,22 +2449,22 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, 32, 32, 8>), grid, dim3(256), 0, s, part_d,  \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
                            st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
-                           np, meta, k, (unsigned long long *)qthr, filt);                         \
+                           np, meta, k, (unsigned long long *)qthr, filt, qperm);                         \
     else if (pf && KP == 32)                                                                     \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, 32, 64, 8>), grid, dim3(256), 0, s, part_d,  \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
                            st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
-                           np, meta, k, (unsigned long long *)qthr, filt);                         \
+                           np, meta, k, (unsigned long long *)qthr, filt, qperm);                         \
     else if (two)                                                                                \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP, 32>), grid, dim3(256), 0, s, part_d,     \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
                            st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
-                           np, meta, k, (unsigned long long *)qthr, filt);                         \
+                           np, meta, k, (unsigned long long *)qthr, filt, qperm);                         \
     else                                                                                         \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP, 64>), grid, dim3(256), 0, s, part_d,     \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
                            st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
-                           np, meta, k, (unsigned long long *)qthr, filt);                         \
+                           np, meta, k, (unsigned long long *)qthr, filt, qperm);                         \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);
 #undef CALL

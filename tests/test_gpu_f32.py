@@ -292,3 +292,22 @@ def test_gemm_state_holds_near_ties(knn, oracle):
     assert mode == 1   # GEMM
     assert_same(got, oracle.knn(X, 30), "near-tie crowd f64")
     assert u == 0, u
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_gemm_merge_query_order(knn, oracle, monkeypatch, dtype):
+    """The GEMM-mode merge in the query order of knn_order.hip (label
+    propagation over the lists' heads, then a radix sort; forced with
+    KNN_ORDER=1 -- by default only past 64 MB blocks) gives the same bytes
+    as the merge in index order, and the oracle's neighbours."""
+    X, _ = datasets.mnist_real(3000, 200)
+    if dtype == "f32":
+        X = rounded(X)
+    monkeypatch.setenv("KNN_ORDER", "1")
+    got, mode, _ = run_engine(X, 30, dtype=dtype)
+    assert mode == 1
+    monkeypatch.delenv("KNN_ORDER")
+    monkeypatch.setenv("KNN_NO_ORDER", "1")
+    base, _, _ = run_engine(X, 30, dtype=dtype)
+    assert got.tobytes() == base.tobytes()
+    assert_same(got, oracle.knn(X, 30), "ordered merge %s" % dtype)
