@@ -964,10 +964,10 @@ static int find_order(knn_ctx_t *c, int set, int nsplit)
             return KNN_ERR_NOMEM;
         c->ord_cap = c->nq_pad;
     }
-    /* 6 rounds: labels settle to cluster-sized pieces (pointer jumping
+    /* 4 rounds: labels settle to cluster-sized pieces (pointer jumping
      * halves the distance to the piece's minimum each round) */
     RCHK(knn_launch_order(c->part_i[set], nsplit, c->lpq, c->klx, (int)c->nq, (int)c->nq_pad,
-                          (long long)c->q_base, 6, c->ord_lab, c->ord_keys, c->ord_iota, c->ord_perm, c->ord_tmp,
+                          (long long)c->q_base, 4, c->ord_lab, c->ord_keys, c->ord_iota, c->ord_perm, c->ord_tmp,
                           c->ord_tmp_bytes, c->ms));
     c->ord_ready = 1;
     return KNN_OK;

@@ -325,10 +325,10 @@ __device__ __forceinline__ int knn_spec8(T v)
 // col-major source (the .mat layout): a workgroup owns 64 rows and walks the
 // columns in 64 x 64 tiles (each wave reads 64 consecutive rows of a column:
 // 512-byte runs), all 16 loads of a thread's tile in flight before their
-// conversion, and the next tile's 16 issued before this one is converted
-// (32 in flight); bytes go through LDS into 16-byte row stores.  Thread
-// (ty, tx) sums row tx's squares over columns = ty mod 4; four partials a
-// row.
+// conversion; bytes go through LDS into 16-byte row stores.  Thread (ty, tx)
+// sums row tx's squares over columns = ty mod 4; four partials a row.
+// (Issuing the next tile's 16 loads before converting this one -- 32 in
+// flight -- measured slower: 106 -> 130 us for MNIST, rocprofv3.)
 template <typename T, typename S>
 __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst, size_t rows, size_t rows_pad,
                                                    int n, int rs, const S *__restrict__ src, size_t ld)
@@ -346,18 +346,12 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
     knn_meta_acc ma;
     double s = 0.0;
     unsigned si = 0u;
-    S v[16];
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-        const int j = ty + 4 * e;
-        v[e] = (live && j < n) ? __builtin_nontemporal_load(xp + (size_t)j * ld) : (S)0;
-    }
     for (int j0 = 0; j0 < rs; j0 += 64) {
-        S vn[16];
+        S v[16];
 #pragma unroll
         for (int e = 0; e < 16; e++) {
-            const int j = j0 + 64 + ty + 4 * e;
-            vn[e] = (live && j < n) ? __builtin_nontemporal_load(xp + (size_t)j * ld) : (S)0;
+            const int j = j0 + ty + 4 * e;
+            v[e] = (live && j < n) ? __builtin_nontemporal_load(xp + (size_t)j * ld) : (S)0;
         }
 #pragma unroll
         for (int e = 0; e < 16; e++) {
@@ -379,8 +373,6 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
             *(knn_v4i *)(dst + (i0 + r) * (size_t)rs + j0 + c0) = (knn_v4i){(int)w4[0], (int)w4[1], (int)w4[2], (int)w4[3]};
         }
         __syncthreads();
-#pragma unroll
-        for (int e = 0; e < 16; e++) v[e] = vn[e];
     }
     part[ty][tx] = s;
     ipart[ty][tx] = si;
