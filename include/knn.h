@@ -34,6 +34,9 @@
  *   KNN_NO_QSUM=1         int8 kernels without the cross-split summaries
  *   KNN_I8_W8=1           12-entry int8 lists on the 8-wave kernel (128-row
  *                         tiles) instead of the 64-row half-tile kernel
+ *   KNN_ORDER=1 / KNN_NO_ORDER=1
+ *                         GEMM-mode merge in the clustered query order
+ *                         (default past 64 MB blocks) / always index order
  *   KNN_I8_QG1=1          one query group a wave on rows of <= 128 bytes
  *                         (the half-tile kernel otherwise carries two: 256
  *                         queries a workgroup sharing each staged row)
