@@ -120,3 +120,18 @@ def test_i8_lane_list_lengths(oracle, monkeypatch, kl, case):
         check(oracle, X, 30)
     else:
         check(oracle, datasets.sift_like(8000, 128, clusters=16, seed=3), 32, dtype="f32")
+
+
+@pytest.mark.parametrize("m,k", [(1000, 32), (777, 10)])
+def test_i8_two_query_groups_match_one(oracle, monkeypatch, m, k):
+    """Rows of <= 4 K-steps run two query groups a wave (256-query
+    workgroups, knn_i8_qg): a partial last block of 256 queries, bit-exact
+    vs the oracle and byte-identical to the one-group kernel
+    (KNN_I8_QG1=1)."""
+    X = datasets.sift_like(m, 128).astype(np.float64)
+    check(oracle, X, k)
+    got2, _ = run_engine(X, k, "f64")
+    monkeypatch.setenv("KNN_I8_QG1", "1")
+    got1, b = run_engine(X, k, "f64")
+    assert b == 8
+    assert got1.tobytes() == got2.tobytes()
