@@ -111,6 +111,8 @@ struct knn_ctx {
      * with 65-entry lane lists and its buffers */
     double hmeta[KNN_META_DOUBLES];
     int have_hmeta;
+    int split_solo;           /* choose_splits: this step folds the search's own query
+                               * byte block first (a P = 1 search is only that) */
     int sub_research;         /* this context is such a sub-context: 65-entry lists
                                * over the most splits the merge takes */
     int one_block_q8;         /* the search's only step folded its own query byte block */
@@ -822,8 +824,17 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         /* the half-tile kernel's 2 lists a split see twice the rows a lane (long rows):
          * it takes 5(k+1)/KL lists a query (MNIST P = 1, uncertified
          * queries a pass: 58 at 4 splits, 2 at 6, 0 at 7; SIFT 334 at 5) */
-        const int kl = c->klx, f = (c->i8_wgpc == 2 && knn_s8_rs(c->n) / 32 > 8) ? 5 : 3;
-        s_min = (f * (c->k + 1) + c->lpq * kl - 1) / (c->lpq * kl);
+        /* (in halves) short rows on the two-group kernel folding the own
+         * query block: 2.5 (k+1)/KL -- a P = 1 search's uncertified
+         * queries go to the int8 re-search (SIFT P = 1 emulated: 4 splits
+         * 167.5 ms, 5 splits 170.3 ms, both 0 uncertified after it; a
+         * ring's fused launch keeps 3: at P = 8 4 splits left 192 a pass
+         * for the rescan, 5 splits 27) */
+        const int kl = c->klx;
+        const int f2 = (c->i8_wgpc == 2 && knn_s8_rs(c->n) / 32 > 8)
+                           ? 10
+                           : (c->split_solo && knn_i8_qg(c->klx, c->lpq, c->n) == 2 ? 5 : 6);
+        s_min = (f2 * (c->k + 1) + 2 * c->lpq * kl - 1) / (2 * c->lpq * kl);
         if (s_min > smax) s_min = smax;
         if (s_min < 1) s_min = 1;
     }
@@ -1095,6 +1106,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     if (!d_cblock) d_cblock = d_sblock;   /* INT mode: k_merge never reads its rows */
     HIPCHK(hipSetDevice(c->device));
     RCHK(flush_pend2(c, NULL, NULL));   /* a deferred merge goes first, in step order */
+    c->split_solo = c->i8 && c->nstep == 0 && !xb && d_sblock != NULL && d_sblock == c->q8 && nc == c->nq;
     const int nsplit = choose_splits(c, nc);
     const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
     c->nsplit_last = nsplit;
