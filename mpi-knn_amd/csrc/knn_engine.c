@@ -749,7 +749,12 @@ static size_t split_bytes(const knn_ctx_t *c)
  * Calibrated on the emulated ring (tools/ring_emulate.py, KNN_SPLITS sweeps):
  * mnist P = 2 / 4 / 8 best at 1-3 / 1-2 / 4 splits, sift P = 4 / 8 at 1. */
 #define KNN_WG_COST_I8_KSTEPS 60.0
-#define KNN_MERGE_COST 1e-6    /* k_merge per (query, split), in tiles      */
+/* k_merge per (query, split), in tile times: the GEMM merge re-ranks with
+ * exact S, ~4.3 ns a (query, split) against a 27 us split-fp16 tile
+ * (emulated mnist-real P = 2: 4 / 13 splits 1.03 / 2.19 ms of exposed
+ * merge; 1e-6 here had the model pick 13 splits at P = 2 and 4, where 4-6
+ * run 6-7% faster) */
+#define KNN_MERGE_COST 1.6e-4
 /* int8 kernel: k_merge's exposed time grows ~1.2e-4 tile times per (query,
  * split) (emulated P = 8 fused launch: 13 splits 0.10 ms against 4 splits
  * 0.06 ms of exposed merge at 7500 queries) */
