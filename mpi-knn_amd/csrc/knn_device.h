@@ -102,8 +102,9 @@ __device__ __forceinline__ int i8_norm_pos(int r)
 //     IW(r) = -floor(|x'|^2 / 2)
 // is where the row's MFMA accumulators start (the C operand of a tile's
 // first K-step), so with A = q'.c' the accumulator ends at
-//     acc = A + IW = (|q'|^2 - d^2 - p) / 2,   p = |x'|^2 & 1,
-// and the epilogue filters on acc alone: 2 acc >= |q'|^2 - lim admits every
+//     acc = A + IW = (|q'|^2 - d^2 + p) / 2,   p = |x'|^2 & 1
+// (A = (|q'|^2 + |x'|^2 - d^2) / 2, IW = -(|x'|^2 - p) / 2), and the epilogue
+// filters on acc alone: 2 acc >= |q'|^2 - lim <=> d^2 <= lim + p admits every
 // candidate with d^2 <= lim (and some with d^2 = lim + 1) without one VALU
 // operation per candidate.  The slot word
 //     K2(r) = 31 - slot(r) - 32 p,

@@ -102,7 +102,7 @@ struct knn_ctx {
      * a direct-exchange pass alternates two launch sizes, and one model
      * evaluation costs ~0.5 ms of host time at 15000 queries */
 #define KNN_SPLIT_CACHE 8
-    struct { size_t nc; int lpq, i8, best; } split_cache[KNN_SPLIT_CACHE];
+    struct { size_t nc; int lpq, i8, solo, klx, best; } split_cache[KNN_SPLIT_CACHE];
     int split_next;
     int nfail;
     int mode;
@@ -787,7 +787,8 @@ static double launch_makespan(long nqb, long ntiles, int s, int cus, double wgc)
 /* Corpus splits per query block: the count with the smallest modelled
  * launch makespan plus merge cost (each split adds a partial list per
  * query), keeping >= 4 tiles per split and the partial lists within
- * KNN_PART_BUDGET.  Cached per corpus block size. */
+ * KNN_PART_BUDGET.  Cached per (corpus block size, lists a query, kernel,
+ * own-block step, lane-list length): each of these changes s_min. */
 static int choose_splits(knn_ctx_t *c, size_t nc)
 {
     const char *env = getenv("KNN_SPLITS");
@@ -808,7 +809,8 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     }
     for (int e = 0; e < KNN_SPLIT_CACHE; e++)
         if (c->split_cache[e].best > 0 && c->split_cache[e].nc == nc && c->split_cache[e].lpq == c->lpq &&
-            c->split_cache[e].i8 == c->i8)
+            c->split_cache[e].i8 == c->i8 && c->split_cache[e].solo == c->split_solo &&
+            c->split_cache[e].klx == c->klx)
             return c->split_cache[e].best;
     int smax = KNN_MAX_LISTS / c->lpq;
     const size_t per = split_bytes(c);
@@ -873,6 +875,8 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         c->split_cache[e].nc = nc;
         c->split_cache[e].lpq = c->lpq;
         c->split_cache[e].i8 = c->i8;
+        c->split_cache[e].solo = c->split_solo;
+        c->split_cache[e].klx = c->klx;
         c->split_cache[e].best = best;
         return best;
     }
@@ -888,6 +892,8 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     c->split_cache[e].nc = nc;
     c->split_cache[e].lpq = c->lpq;
     c->split_cache[e].i8 = c->i8;
+    c->split_cache[e].solo = c->split_solo;
+    c->split_cache[e].klx = c->klx;
     c->split_cache[e].best = best;
     return best;
 }
@@ -1384,6 +1390,9 @@ static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
     RCHK(ctx_end_device(u, c->sub_out, s));
     RCHK(knn_launch_resolve8(c->sub_flag, c->fail_list, nf, u->fail_list, u->fail_count, c->sub_out, c->k, d_out,
                              c->fail_list2, c->fail_count, s));
+    /* (tests: a failure at this point, after resolve8 rewrote rows of d_out
+     * and the device count -- knn_ctx_end's fallback must still be exact) */
+    if (env_on("KNN_TEST_RESEARCH8_FAIL")) return KNN_ERR_HIP;
     int nn = 0;
     HIPCHK(hipMemcpyAsync(&nn, c->fail_count, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -1450,8 +1459,14 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     c->mode = host[1];
     if (c->nfail > 0 && research8(c, d_out, s) != KNN_OK) {
         /* the re-search is an optimisation: on any failure of it the exact
-         * rescan resolves the same queries (the fail list is untouched until
-         * research8's last step, which cannot fail) */
+         * rescan resolves the same queries.  The rescan reads only the host
+         * count c->nfail and c->fail_list, both still the first pass's
+         * (resolve8 writes the new list into fail_list2; they are swapped
+         * only after the count's read-back succeeded).  What resolve8 may
+         * already have changed is harmless: the d_out rows it rewrote are
+         * rows of failed queries, which the rescan rewrites again, and the
+         * device fail_count is read by nothing after this point and reset by
+         * the next begin.  (test_gpu_s8.py injects this failure.) */
         HIPCHK(hipStreamSynchronize(s));
         (void)hipGetLastError();
     }

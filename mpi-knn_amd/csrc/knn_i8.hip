@@ -655,8 +655,8 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     int nc = 0, e_t0 = 0, e_t1 = 0, e_b = 0;
     // Survivors are the candidates with d^2 <= lim = min(own KL-th, shared
     // bound).  The accumulators started at the rows' init words, so acc =
-    // (|q'|^2 - d^2 - p) / 2 (i8_init_word): the filter 2 acc >= |q'|^2 -
-    // lim, i.e. acc >= Ta = ceil((|q'|^2 - lim) / 2), admits all of them
+    // (|q'|^2 - d^2 + p) / 2 (i8_init_word): the filter 2 acc >= |q'|^2 -
+    // lim <=> d^2 <= lim + p, i.e. acc >= Ta = ceil((|q'|^2 - lim) / 2), admits all of them
     // (and rows with d^2 = lim + 1, p = 1), straight off the MFMA output.
     // Lanes that pass build the exact keys v = 64 acc + K2 and select with
     // v >= T = 32 (|q'|^2 - lim).  An empty list (lim = INF) admits every

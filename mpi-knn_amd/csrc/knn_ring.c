@@ -27,11 +27,15 @@
  * fp16 rows: knn_ctx_shadow) and element blocks otherwise; the exact rescan
  * always reads element blocks.
  *
- * The hop is a transport: RCCL over the node's GPUs, or (KNN_RING_LOOPBACK=1)
+ * The hop is a transport: RCCL over the node's GPUs; or (KNN_RING_LOOPBACK=1)
  * a loopback of P virtual ranks on device 0 whose transfers are device
- * copies on one "fabric" stream -- the same schedules, buffers, events and
- * lag rule, so the P >= 2 ring is testable on a one-GPU box
- * (tests/test_gpu_parity.py).
+ * copies on one "fabric" stream; or (KNN_RING_LOOPBACK=rccl) the same P
+ * virtual ranks whose every transfer is an RCCL send to self and receive
+ * from self on a one-device communicator (ncclCommInitAll with ndev = 1),
+ * grouped exactly as the RCCL transport groups a hop or an exchange.  The
+ * schedules, buffers, events and lag rule are the same for all three, so the
+ * P >= 2 ring -- and its RCCL calls -- run on a one-GPU box
+ * (tests/test_gpu_parity.py, tests/test_gpu_rccl_self.py).
  */
 #include "knn_internal.h"
 
@@ -44,11 +48,20 @@
 #define KNN_RING_MAX 64
 #define NRX (KNN_STEP_LAG + 2)  /* receive buffers per device */
 
-enum { RING_RCCL = 0, RING_LOOPBACK = 1 };
+enum { RING_RCCL = 0, RING_LOOPBACK = 1, RING_SELF = 2 };
 typedef struct {
     int kind;
-    hipStream_t fabric;         /* loopback: every hop's copies, in hop order */
+    hipStream_t fabric;         /* loopback / self: every hop's transfers, in hop order */
+    ncclComm_t self;            /* RING_SELF: the one-device communicator */
+    uint32_t *stall_h;          /* KNN_RING_TEST_STALL (loopback): the fabric stream */
+    void *stall_d;              /*   waits on this word before its first transfer */
 } ring_transport_t;
+
+/* Progress marks: every fold and every transfer group records one (on the
+ * stream it ran on); ring_drain's deadline restarts whenever one more of
+ * them has completed, so KNN_RING_TIMEOUT_S bounds the time with no fold and
+ * no transfer finishing -- a transfer that never lands -- not a pass. */
+#define MK_MAX (2 * KNN_RING_MAX + 8)
 
 typedef struct {
     int dev;
@@ -68,8 +81,16 @@ typedef struct {
     knn_ctx_t *ctx;
     hipStream_t cs, ms;         /* compute / comm streams */
     hipEvent_t ev_comp, ev_comm;
+    hipEvent_t mk[MK_MAX];      /* progress marks (nmk recorded since the last drain) */
+    int nmk, mkn;               /* recorded since the last drain / created */
     ncclComm_t comm;
 } ring_dev_t;
+
+static int ring_mark(ring_dev_t *e, hipStream_t s)
+{
+    if (e->nmk >= e->mkn) return KNN_OK;   /* (a pass records at most 2P) */
+    return hipEventRecord(e->mk[e->nmk++], s) == hipSuccess ? KNN_OK : KNN_ERR_HIP;
+}
 
 static double now_s(void)
 {
@@ -78,27 +99,58 @@ static double now_s(void)
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-/* Loopback hop: virtual rank g's cur -> rank g+1's nxt, all on device 0.
- * The fabric stream waits for every rank's compute-side event (its nxt is
- * free, its own block is packed) and runs the copies in hop order, so a
- * block forwarded at hop h was received at hop h-1 on the same stream. */
+/* KNN_RING_TEST_STALL=1 (loopback transport, tests): the fabric stream
+ * waits on a host word nobody sets before its transfers, so they never
+ * land; ring_drain's timeout sets it when it gives up.  No kernel spins: the
+ * wait is the stream's own, and the queue drains once the word is set. */
+static int ring_stall_hook(ring_transport_t *t)
+{
+    if (!t->stall_d) return KNN_OK;
+    return hipStreamWaitValue32(t->fabric, t->stall_d, 1, hipStreamWaitValueGte, 0xffffffffu) == hipSuccess
+               ? KNN_OK
+               : KNN_ERR_HIP;
+}
+
+/* Loopback / self hop: virtual rank g's cur -> rank g+1's nxt, all on
+ * device 0.  The fabric stream waits for every rank's compute-side event
+ * (its nxt is free, its own block is packed) and runs the transfers in hop
+ * order, so a block forwarded at hop h was received at hop h-1 on the same
+ * stream.  The loopback copies; the self transport moves every block through
+ * RCCL (send to self, receive from self). */
 static int ring_hop_loopback(ring_dev_t *d, int P, size_t bytes, ring_transport_t *t)
 {
+    int rc;
     if (hipSetDevice(d[0].dev) != hipSuccess) return KNN_ERR_HIP;
     for (int g = 0; g < P; g++)
         if (hipStreamWaitEvent(t->fabric, d[g].ev_comp, 0) != hipSuccess) return KNN_ERR_HIP;
+    if ((rc = ring_stall_hook(t))) return rc;
+    if (t->kind == RING_SELF) {
+        /* one group, as the RCCL transport's hop: P sends to self and P
+         * receives from self on one communicator, matched in posting order
+         * (send g pairs with the receive into rank g+1's nxt) */
+        if (ncclGroupStart() != ncclSuccess) return KNN_ERR_RCCL;
+        for (int g = 0; g < P; g++)
+            if (ncclSend(d[g].cur, bytes, ncclUint8, 0, t->self, t->fabric) != ncclSuccess ||
+                ncclRecv(d[(g + 1) % P].nxt, bytes, ncclUint8, 0, t->self, t->fabric) != ncclSuccess) {
+                ncclGroupEnd();
+                return KNN_ERR_RCCL;
+            }
+        if (ncclGroupEnd() != ncclSuccess) return KNN_ERR_RCCL;
+    } else {
+        for (int g = 0; g < P; g++)
+            if (hipMemcpyAsync(d[(g + 1) % P].nxt, d[g].cur, bytes, hipMemcpyDeviceToDevice, t->fabric) !=
+                hipSuccess)
+                return KNN_ERR_HIP;
+    }
     for (int g = 0; g < P; g++)
-        if (hipMemcpyAsync(d[(g + 1) % P].nxt, d[g].cur, bytes, hipMemcpyDeviceToDevice, t->fabric) !=
-            hipSuccess)
+        if (hipEventRecord(d[g].ev_comm, t->fabric) != hipSuccess || ring_mark(&d[g], t->fabric))
             return KNN_ERR_HIP;
-    for (int g = 0; g < P; g++)
-        if (hipEventRecord(d[g].ev_comm, t->fabric) != hipSuccess) return KNN_ERR_HIP;
     return KNN_OK;
 }
 
 static int ring_hop(ring_dev_t *d, int P, size_t bytes, ring_transport_t *t)
 {
-    if (t->kind == RING_LOOPBACK) return ring_hop_loopback(d, P, bytes, t);
+    if (t->kind != RING_RCCL) return ring_hop_loopback(d, P, bytes, t);
     /* nxt[g] was read by step s-1's compute: the comm waits for it. */
     for (int g = 0; g < P; g++) {
         if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
@@ -115,19 +167,25 @@ static int ring_hop(ring_dev_t *d, int P, size_t bytes, ring_transport_t *t)
     if (ncclGroupEnd() != ncclSuccess) return KNN_ERR_RCCL;
     for (int g = 0; g < P; g++) {
         if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
-        if (hipEventRecord(d[g].ev_comm, d[g].ms) != hipSuccess) return KNN_ERR_HIP;
+        if (hipEventRecord(d[g].ev_comm, d[g].ms) != hipSuccess || ring_mark(&d[g], d[g].ms))
+            return KNN_ERR_HIP;
     }
     return KNN_OK;
 }
 
 /* Bounded wait (KNN_RING_TIMEOUT_S, default 300 s) for one stream of every
- * device: `comm` = the comm streams (every transfer of a pass), else the
- * compute streams (the meta all-reduce runs there).  RCCL: polls each
- * communicator's asynchronous error beside the streams, and on an error or
- * the deadline aborts every communicator (the caller then skips
- * ncclCommDestroy) and returns KNN_ERR_RCCL -- a dead peer or a transfer that
- * never completes ends the search with a status instead of a hang in a
- * later stream synchronisation.  Loopback: the fabric stream. */
+ * device: `comm` = the transfers (the comm streams, or the fabric stream of
+ * the loopback / self transports), else the compute streams (the meta
+ * all-reduce runs there).  The bound is on progress, not on the pass: the
+ * deadline restarts whenever another of the pass's progress marks (one per
+ * fold and per transfer group, ring_mark) completes, so a long compute tail
+ * of many folds never trips it, a transfer that never lands does.  RCCL and
+ * self: polls each communicator's asynchronous error beside the streams, and
+ * on an error or the deadline aborts every communicator (the caller then
+ * skips ncclCommDestroy and every stream synchronisation) and returns
+ * KNN_ERR_RCCL -- a dead peer or a stuck transfer ends the search with a
+ * status instead of a hang in a later synchronisation.  Loopback: the same
+ * status, with the stream synchronisations skipped likewise. */
 static double ring_timeout_s(void)
 {
     const char *e = getenv("KNN_RING_TIMEOUT_S");
@@ -135,12 +193,24 @@ static double ring_timeout_s(void)
     return v > 0.0 ? v : 300.0;
 }
 
+static int ring_marks_done(ring_dev_t *d, int P)
+{
+    int done = 0;
+    for (int g = 0; g < P; g++) {
+        if (hipSetDevice(d[g].dev) != hipSuccess) return -1;
+        for (int x = 0; x < d[g].nmk; x++) done += hipEventQuery(d[g].mk[x]) == hipSuccess;
+    }
+    return done;
+}
+
 static int ring_drain(ring_dev_t *d, int P, ring_transport_t *t, int comm, int *aborted)
 {
-    const double deadline = now_s() + ring_timeout_s();
+    const double tmo = ring_timeout_s();
+    double deadline = now_s() + tmo;
+    int marks = ring_marks_done(d, P);
     for (;;) {
         int pending = 0, bad = 0;
-        if (t->kind == RING_LOOPBACK && comm) {
+        if (t->kind != RING_RCCL && comm) {
             if (hipSetDevice(d[0].dev) != hipSuccess) return KNN_ERR_HIP;
             const hipError_t q = hipStreamQuery(t->fabric);
             if (q == hipErrorNotReady) pending = 1;
@@ -159,14 +229,36 @@ static int ring_drain(ring_dev_t *d, int P, ring_transport_t *t, int comm, int *
                 }
             }
         }
-        if (!pending && !bad) return KNN_OK;
+        if (t->kind == RING_SELF && t->self) {
+            ncclResult_t st = ncclSuccess;
+            if (ncclCommGetAsyncError(t->self, &st) != ncclSuccess ||
+                (st != ncclSuccess && st != ncclInProgress))
+                bad = 1;
+        }
+        if (!pending && !bad) {
+            for (int g = 0; g < P; g++) d[g].nmk = 0;   /* every mark has completed */
+            return KNN_OK;
+        }
+        const int now_marks = ring_marks_done(d, P);
+        if (now_marks > marks) {
+            marks = now_marks;
+            deadline = now_s() + tmo;
+        }
         if (bad || now_s() > deadline) {
             if (t->kind == RING_RCCL) {
                 for (int g = 0; g < P; g++)
                     if (d[g].comm) ncclCommAbort(d[g].comm);
-                *aborted = 1;
+            } else if (t->kind == RING_SELF && t->self) {
+                ncclCommAbort(t->self);
             }
-            return t->kind == RING_RCCL ? KNN_ERR_RCCL : KNN_ERR_HIP;
+            if (t->stall_h) {
+                /* the test hook's stalled transfer: release it, so the
+                 * process ends with its queues drained (tests only) */
+                *(volatile uint32_t *)t->stall_h = 1;
+                __sync_synchronize();
+            }
+            *aborted = 1;
+            return KNN_ERR_RCCL;
         }
         const struct timespec ts = {0, 50000};   /* 50 us */
         nanosleep(&ts, NULL);
@@ -192,17 +284,34 @@ static int fold_one(ring_dev_t *e, const void *blk, size_t rows, size_t base, in
  * group (RCCL) or on the fabric stream (loopback); ev_comm marks arrival. */
 static int direct_exchange(ring_dev_t *d, int P, size_t bytes, void *const *send, ring_transport_t *t)
 {
-    if (t->kind == RING_LOOPBACK) {
+    int rc;
+    if (t->kind != RING_RCCL) {
         if (hipSetDevice(d[0].dev) != hipSuccess) return KNN_ERR_HIP;
         for (int g = 0; g < P; g++)
             if (hipStreamWaitEvent(t->fabric, d[g].ev_comp, 0) != hipSuccess) return KNN_ERR_HIP;
+        if ((rc = ring_stall_hook(t))) return rc;
+        if (t->kind == RING_SELF) {
+            /* the RCCL transport's one group of the whole exchange: P(P-1)
+             * sends to self, each followed by the receive it pairs with */
+            if (ncclGroupStart() != ncclSuccess) return KNN_ERR_RCCL;
+            for (int g = 0; g < P; g++)
+                for (int j = 1; j < P; j++)
+                    if (ncclSend(send[(g - j + P) % P], bytes, ncclUint8, 0, t->self, t->fabric) != ncclSuccess ||
+                        ncclRecv(d[g].rx[j - 1], bytes, ncclUint8, 0, t->self, t->fabric) != ncclSuccess) {
+                        ncclGroupEnd();
+                        return KNN_ERR_RCCL;
+                    }
+            if (ncclGroupEnd() != ncclSuccess) return KNN_ERR_RCCL;
+        } else {
+            for (int g = 0; g < P; g++)
+                for (int j = 1; j < P; j++)
+                    if (hipMemcpyAsync(d[g].rx[j - 1], send[(g - j + P) % P], bytes, hipMemcpyDeviceToDevice,
+                                       t->fabric) != hipSuccess)
+                        return KNN_ERR_HIP;
+        }
         for (int g = 0; g < P; g++)
-            for (int j = 1; j < P; j++)
-                if (hipMemcpyAsync(d[g].rx[j - 1], send[(g - j + P) % P], bytes, hipMemcpyDeviceToDevice,
-                                   t->fabric) != hipSuccess)
-                    return KNN_ERR_HIP;
-        for (int g = 0; g < P; g++)
-            if (hipEventRecord(d[g].ev_comm, t->fabric) != hipSuccess) return KNN_ERR_HIP;
+            if (hipEventRecord(d[g].ev_comm, t->fabric) != hipSuccess || ring_mark(&d[g], t->fabric))
+                return KNN_ERR_HIP;
         return KNN_OK;
     }
     for (int g = 0; g < P; g++) {
@@ -221,7 +330,8 @@ static int direct_exchange(ring_dev_t *d, int P, size_t bytes, void *const *send
     if (ncclGroupEnd() != ncclSuccess) return KNN_ERR_RCCL;
     for (int g = 0; g < P; g++) {
         if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
-        if (hipEventRecord(d[g].ev_comm, d[g].ms) != hipSuccess) return KNN_ERR_HIP;
+        if (hipEventRecord(d[g].ev_comm, d[g].ms) != hipSuccess || ring_mark(&d[g], d[g].ms))
+            return KNN_ERR_HIP;
     }
     return KNN_OK;
 }
@@ -248,6 +358,7 @@ static int direct_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t n, int d
     for (int g = 0; g < P && !fuse_all; g++) {
         if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
         if ((rc = fold_one(&d[g], send[g], d[g].rows, d[g].base, rescan, form))) return rc;
+        if ((rc = ring_mark(&d[g], d[g].cs))) return rc;
     }
     for (int g = 0; g < P && P > 1; g++) {
         ring_dev_t *e = &d[g];
@@ -271,7 +382,7 @@ static int direct_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t n, int d
             for (int j = 1; j < P && !rc; j++) rc = fold_one(e, blk[j], nc[j], base[j], rescan, form);
         }
         if (rc) return rc;
-        if (hipEventRecord(e->ev_comp, e->cs) != hipSuccess) return KNN_ERR_HIP;
+        if (hipEventRecord(e->ev_comp, e->cs) != hipSuccess || ring_mark(e, e->cs)) return KNN_ERR_HIP;
     }
     return KNN_OK;
 }
@@ -308,7 +419,8 @@ static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int
             if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
             rc = fold_one(&d[g], d[g].cur, rows, base, rescan, form);
             if (rc) return rc;
-            if (hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) return KNN_ERR_HIP;
+            if (hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess || ring_mark(&d[g], d[g].cs))
+                return KNN_ERR_HIP;
         }
         if (s < P - 1) {
             for (int g = 0; g < P; g++) {
@@ -366,9 +478,9 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
     ring_transport_t tr;
     memset(&tr, 0, sizeof(tr));
     const char *lb = getenv("KNN_RING_LOOPBACK");
-    tr.kind = (lb && lb[0] == '1') ? RING_LOOPBACK : RING_RCCL;
+    tr.kind = !lb ? RING_RCCL : lb[0] == '1' ? RING_LOOPBACK : strcmp(lb, "rccl") == 0 ? RING_SELF : RING_RCCL;
     /* RCCL: one block per GPU, at most the GPUs present (procs > GPUs runs on
-     * every GPU); loopback: P virtual ranks on device 0 */
+     * every GPU); loopback and self: P virtual ranks on device 0 */
     int P = ngpus;
     if (tr.kind == RING_RCCL && P > ndev) P = ndev;
     if (P > KNN_RING_MAX) P = KNN_RING_MAX;
@@ -386,13 +498,27 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
     ncclComm_t comms[KNN_RING_MAX];
     memset(comms, 0, sizeof(comms));
     int rc = KNN_OK, aborted = 0;
-    for (int g = 0; g < P; g++) devs[g] = tr.kind == RING_LOOPBACK ? 0 : g;
+    for (int g = 0; g < P; g++) devs[g] = tr.kind == RING_RCCL ? g : 0;
     if (tr.kind == RING_RCCL) {
         if (ncclCommInitAll(comms, P, devs) != ncclSuccess) return KNN_ERR_RCCL;
     } else {
         if (hipSetDevice(0) != hipSuccess ||
             hipStreamCreateWithFlags(&tr.fabric, hipStreamNonBlocking) != hipSuccess)
             return KNN_ERR_HIP;
+        if (tr.kind == RING_SELF && ncclCommInitAll(&tr.self, 1, devs) != ncclSuccess) {
+            hipStreamDestroy(tr.fabric);
+            return KNN_ERR_RCCL;
+        }
+        const char *st = getenv("KNN_RING_TEST_STALL");
+        if (tr.kind == RING_LOOPBACK && st && st[0] == '1') {
+            if (hipHostMalloc((void **)&tr.stall_h, 64, hipHostMallocMapped | hipHostMallocCoherent) !=
+                    hipSuccess ||
+                hipHostGetDevicePointer(&tr.stall_d, tr.stall_h, 0) != hipSuccess) {
+                hipStreamDestroy(tr.fabric);
+                return KNN_ERR_NOMEM;
+            }
+            tr.stall_h[0] = 0;
+        }
     }
 
     for (int g = 0; g < P && !rc; g++) {
@@ -409,6 +535,12 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             rc = KNN_ERR_HIP;
             break;
         }
+        for (e->mkn = 0; e->mkn < 2 * P + 8 && e->mkn < MK_MAX; e->mkn++)
+            if (hipEventCreateWithFlags(&e->mk[e->mkn], hipEventDisableTiming) != hipSuccess) {
+                rc = KNN_ERR_HIP;
+                break;
+            }
+        if (rc) break;
         const int rx_ok = (e->rx = (void **)calloc((size_t)nrx, sizeof(void *))) != NULL;
         if (!rx_ok || hipMalloc(&e->qb, bytes) != hipSuccess ||
             hipMalloc((void **)&e->src, e->rows * n * sizeof(double)) != hipSuccess ||
@@ -475,6 +607,14 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         for (int g = 0; g < P && !rc; g++)
             if (hipMemcpyAsync(d[g].meta, hm, sizeof(hm), hipMemcpyHostToDevice, d[g].cs) != hipSuccess)
                 rc = KNN_ERR_HIP;
+        /* self: each virtual rank's reduced meta once more through
+         * ncclAllReduce(max) on the one-device communicator (the identity
+         * over one rank: the call the RCCL transport makes, on its stream) */
+        for (int g = 0; g < P && !rc && tr.kind == RING_SELF; g++)
+            if (ncclAllReduce(d[g].meta, d[g].meta, KNN_META_DOUBLES, ncclFloat64, ncclMax, tr.self,
+                              d[g].cs) != ncclSuccess)
+                rc = KNN_ERR_RCCL;
+        if (!rc && tr.kind == RING_SELF) rc = ring_drain(d, P, &tr, 0, &aborted);
     }
     /* the form blocks travel in: the search's shadow form when it has one
      * (P > 1; KNN_NO_SHADOW_RING=1 keeps element blocks) */
@@ -548,12 +688,13 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
             rc = KNN_ERR_HIP;
     }
 
-    for (int g = 0; g < P && !aborted; g++) {
+    for (int g = 0; g < P && (!aborted || tr.stall_h); g++) {
         hipSetDevice(d[g].dev);
         if (d[g].cs) hipStreamSynchronize(d[g].cs);
         if (d[g].ms) hipStreamSynchronize(d[g].ms);
     }
-    if (tr.fabric) hipStreamSynchronize(tr.fabric);
+    /* (a stalled test transfer was released when the drain gave up) */
+    if (tr.fabric && (!aborted || tr.stall_h)) hipStreamSynchronize(tr.fabric);
     for (int g = 0; g < P; g++) {
         hipSetDevice(d[g].dev);
         if (d[g].ctx) knn_ctx_destroy(d[g].ctx);
@@ -566,10 +707,14 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         hipFree(d[g].d_out);
         if (d[g].ev_comp) hipEventDestroy(d[g].ev_comp);
         if (d[g].ev_comm) hipEventDestroy(d[g].ev_comm);
+        for (int x = 0; x < MK_MAX; x++)
+            if (d[g].mk[x]) hipEventDestroy(d[g].mk[x]);
         if (d[g].cs) hipStreamDestroy(d[g].cs);
         if (d[g].ms) hipStreamDestroy(d[g].ms);
         if (tr.kind == RING_RCCL && comms[g] && !aborted) ncclCommDestroy(comms[g]);
     }
+    if (tr.self && !aborted) ncclCommDestroy(tr.self);
     if (tr.fabric) hipStreamDestroy(tr.fabric);
+    if (tr.stall_h) hipHostFree(tr.stall_h);
     return rc;
 }

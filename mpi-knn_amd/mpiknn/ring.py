@@ -37,13 +37,18 @@ under gloo.
 
 Failures: a peer that dies or stalls must not hang the survivors.  Every
 exchange is waited for with a bound (KNN_RING_TIMEOUT_S, default 300 s; a
-full-size P = 8 pass moves ~50 MB a rank and takes milliseconds): under gloo
-each request's wait carries that timeout; under nccl (RCCL) the wait stays
-a stream-ordered one -- a host-blocking wait would stall the launch queue
-behind the transfers -- and the bound is the process group's own timeout,
-which bench.py sets from the same variable at init_process_group (the RCCL
-watchdog aborts the communicator when it expires).  Either way the caller
-gets RingError, not a hang (tests/test_ring_cpu.py injects a stalled peer).
+full-size P = 8 pass moves ~50 MB a rank and takes milliseconds).  Under
+gloo each request's wait carries that timeout, and a failed or stalled peer
+raises RingError on the survivors (tests/test_ring_cpu.py injects a stalled
+peer).  Under nccl (RCCL) the wait stays a stream-ordered one -- a
+host-blocking wait would stall the launch queue behind the transfers -- so
+a stalled transfer does not raise here: the bound is the process group's
+own timeout, which bench.py sets from the same variable at
+init_process_group, and when it expires the RCCL watchdog aborts the
+communicator and tears the process down with a non-zero exit (no hang,
+but no RingError either).  Errors the nccl work reports at wait() time
+still raise RingError.  The nccl branch runs on one GPU through a
+world-size-1 RCCL group (tests/test_gpu_rccl_self.py).
 """
 import datetime
 import os

@@ -234,6 +234,16 @@ def test_int8_research_of_uncertified(knn, oracle, monkeypatch):
         assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), mode
     assert counts["off"] > 0, counts
     assert counts["on"] < counts["off"], counts
+    # the re-search failing after k_resolve8 has rewritten rows
+    # and the device count -- the exact rescan of the first pass's list
+    # still gives the oracle's result
+    monkeypatch.setenv("KNN_TEST_RESEARCH8_FAIL", "1")
+    e = ring.GpuEngine(torch, 0, n, m, m, 30)
+    e.pack(torch.from_numpy(np.ascontiguousarray(X)).to("cuda:0"), layout_col=False)
+    assert ring.ring_search(None, torch, e, 0, 1, m, 0) > 0   # the first pass's count, not the re-search's
+    got = e.result()
+    assert np.array_equal(got["idx"], ref["idx"])
+    assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64))
 
 
 @pytest.mark.parametrize("dtype,k", [("f64", 30), ("f32", 64)])
