@@ -354,6 +354,20 @@ KNN_API int knn_ctx_end(knn_ctx_t *ctx, knn_neighbour_t *d_out, size_t *unresolv
 KNN_API int knn_ctx_rescan_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
                         size_t c_base, void *stream);
 KNN_API int knn_ctx_rescan_end(knn_ctx_t *ctx, knn_neighbour_t *d_out, void *stream);
+/* A ring rank's int8 re-search, between knn_ctx_end and the rescan pass:
+ * the queries knn_ctx_end left uncertified are searched again on the int8
+ * contraction with 65-entry lane lists (as a single-block search does inside
+ * knn_ctx_end) against the nblk byte blocks the rank still holds (d_sblocks:
+ * its own and the received ones, nc[b] rows from global id c_base[b] --
+ * together every row of the corpus); certified queries get their records
+ * in d_out.  *unresolved (host; the call synchronises the stream) is the
+ * count the rescan pass still has to resolve -- 0 spares the rank the
+ * element-block exchange of mpi-knn-parallel_blocking.c:187-214's repeat.
+ * A no-op (returning the unchanged count) unless the search ran on the int8
+ * contraction in INT mode (knn_ctx_shadow == 2) with k <= 32. */
+KNN_API int knn_ctx_research_blocks(knn_ctx_t *ctx, int nblk, const void *const *d_sblocks, const size_t *nc,
+                                    const size_t *c_base, knn_neighbour_t *d_out, size_t *unresolved,
+                                    void *stream);
 
 /* Convenience: the whole single-device pipeline on one packed block of
  * capacity m (queries == corpus == rows 0..m-1), including the rescan pass

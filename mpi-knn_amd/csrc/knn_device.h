@@ -49,6 +49,38 @@ __device__ __forceinline__ void glds4(const void *src, unsigned lds_dst)
 }
 
 // ---------------------------------------------------------------------------
+// Mode decision from the max-reduced meta (identical on every rank).
+//   INT : every value an integer and every partial sum of the GEMM form
+//         (norms, dot products, |q|^2+|c|^2, d^2) an integer below 2^p
+//         (p = 53 / 24), so d^2 is exact, bit-identical to the reference's
+//         S, and sqrt is injective on it.  fp64: (2 max|x|)^2 n
+//         <= 2^51; fp32: n max|x|^2 <= 2^23 and n (max - min)^2 <= 2^24.
+//   SCAN: non-finite values or norms near overflow -- no error bound.
+//   GEMM: everything else.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ int knn_mode(const double *meta, int n)
+{
+    if constexpr (sizeof(T) == 8) {
+        if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e290))
+            return KNN_MODE_SCAN;
+        const double lim = 2251799813685248.0 / (4.0 * (double)n);   // 2^51 / 4n
+        double mx = meta[KNN_META_MAXABS];
+        if (meta[KNN_META_NONINT] == 0.0 && mx * mx <= lim) return KNN_MODE_INT;
+        return KNN_MODE_GEMM;
+    } else {
+        if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e37))
+            return KNN_MODE_SCAN;
+        const double mx = meta[KNN_META_MAXABS];
+        const double rg = meta[KNN_META_MAXPOS] + meta[KNN_META_MAXNEG];
+        if (meta[KNN_META_NONINT] == 0.0 && (double)n * mx * mx <= 8388608.0 &&
+            (double)n * rg * rg <= 16777216.0)
+            return KNN_MODE_INT;
+        return KNN_MODE_GEMM;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Register top-KP list: L ascending, insertion after equal keys (the lane's
 // candidates arrive in increasing row order, so this is the reference's
 // stable "lower index first" tie rule).  d >= L[KP-1] (incl. +inf,

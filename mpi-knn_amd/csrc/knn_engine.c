@@ -795,7 +795,9 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     /* (workgroups of 128 qg queries: knn_i8_qg) */
     const long qpw = (long)KNN_TQ * (c->i8 ? knn_i8_qg(c->klx, c->lpq, c->n) : 1);
     const long nqb = (long)((c->nq + qpw - 1) / qpw);
-    const long ntiles = (long)((nc + KNN_TC - 1) / KNN_TC);
+    /* k_dist_split streams 256-row tiles: the model's tile unit is its tile */
+    const long tc = (c->split && !env_on("KNN_SPLIT_V1")) ? KNN_SPLIT_TC : KNN_TC;
+    const long ntiles = (long)((nc + tc - 1) / tc);
     /* the re-search of a few uncertified queries: one query block, so the
      * launch's span is one workgroup's scan -- as many splits as the merge
      * takes (lpq * splits + 1 <= 64 lists) */
@@ -816,12 +818,12 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     const size_t per = split_bytes(c);
     if (per > 0 && KNN_PART_BUDGET / per < (size_t)smax)
         smax = KNN_PART_BUDGET / per > 1 ? (int)(KNN_PART_BUDGET / per) : 1;
-    const double wgc = c->i8 ? KNN_WG_COST_I8_KSTEPS / (double)(knn_s8_rs(c->n) / 32) : KNN_WG_COST;
+    const double wgc = c->i8 ? KNN_WG_COST_I8_KSTEPS / (double)(knn_s8_rs(c->n) / 32) : KNN_WG_COST * KNN_TC / tc;
     /* half-tile int8 kernel: two workgroups a CU, each at about half the
      * rate -- the model's slots double and its tile unit (a workgroup's
      * tile time) with them, so the merge term, priced in tile times, halves */
     const int slots = c->cus * (c->i8 ? c->i8_wgpc : 1);
-    const double mc = (c->i8 ? KNN_MERGE_COST_I8 : KNN_MERGE_COST) / (c->i8 ? c->i8_wgpc : 1);
+    const double mc = (c->i8 ? KNN_MERGE_COST_I8 : KNN_MERGE_COST * KNN_TC / tc) / (c->i8 ? c->i8_wgpc : 1);
     /* int8 lists: at least s_min splits so that a lane list expects <= KL/3
      * of the query's k+1 nearest (lpq lists a split; the block may hold all
      * of them): one split of 17-entry lists over a whole corpus left
@@ -1230,7 +1232,8 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
                                   nsplit, c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad,
                                   c->qthr, c->split ? c->qsp : c->qsh, csh, cn_ptr,
                                   (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0) |
-                                      (c->shadow ? KNN_DIST_SHADOW : 0) | (c->split ? KNN_DIST_SPLIT : 0),
+                                      (c->shadow ? KNN_DIST_SHADOW : 0) | (c->split ? KNN_DIST_SPLIT : 0) |
+                                      (c->split && env_on("KNN_SPLIT_V1") ? KNN_DIST_SPLIT_V1 : 0),
                                   c->split ? (float)(-2.0 / ((double)c->sscale * c->sscale)) : -2.f, ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
     HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
@@ -1346,16 +1349,13 @@ static void research8_free(knn_ctx_t *c)
     c->sub_cap = 0;
 }
 
-static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
+/* The re-search proper: the c->nfail uncertified queries of fail_list
+ * against the byte blocks of xb (NULL: the single-block search's own query
+ * byte block, q8), the sub-search's q_base at q_base_sub (past every row id
+ * of the blocks). */
+static int research8_run(knn_ctx_t *c, int nblk, const void *const *blk, const size_t *bnc, const size_t *bbase,
+                         size_t q_base_sub, knn_neighbour_t *d_out, hipStream_t s)
 {
-    /* INT mode only (c->mode: the device's verdict on the real meta): a
-     * speculative begin (knn_ctx_begin_s8 on a stale host hint) whose data
-     * turned out real-valued fails every query in GEMM mode, and the
-     * sub-search would run GEMM work from a context with no element rows */
-    if (c->mode != KNN_MODE_INT || !c->i8 || c->sub_research || !c->one_block_q8 || c->nstep != 1 || !c->have_hmeta ||
-        c->step0_cbase != c->q_base || c->q_rows_pad != knn_rows_pad(c->block_cap) || c->kp > KNN_KP_M ||
-        env_on("KNN_FORCE_RESCAN") || env_on("KNN_NO_RESEARCH8"))
-        return KNN_OK;
     const int nf = c->nfail;
     if (!c->sub || c->sub_cap < (size_t)nf) {
         research8_free(c);
@@ -1381,10 +1381,25 @@ static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
      * key of every uncertified query in qthr, so the re-search filters with
      * the running answer from its first tile (cold 65-entry lists admitted
      * every row of a lane's first tiles: 682 us for two MNIST queries) */
-    RCHK(ctx_begin(u, NULL, c->sub_q8, c->sub_cap, c->step0_cbase + c->step0_nc, c->meta, c->hmeta, s));
+    RCHK(ctx_begin(u, NULL, c->sub_q8, c->sub_cap, q_base_sub, c->meta, c->hmeta, s));
     RCHK(knn_launch_gather8(c->sub_q8, c->q8, c->fail_list, nf, c->n, c->q_rows_pad, knn_rows_pad(c->sub_cap),
                             c->qthr, u->qthr, s));
-    RCHK(ctx_step_impl(u, NULL, c->q8, c->step0_nc, c->step0_cbase, NULL, s));
+    if (nblk > 0) {
+        /* a ring rank: every block it holds, KNN_I8_MAXBLK to a launch */
+        for (int b0 = 0; b0 < nblk; b0 += KNN_I8_MAXBLK) {
+            knn_i8_blocks_t t;
+            memset(&t, 0, sizeof(t));
+            t.nblk = nblk - b0 < KNN_I8_MAXBLK ? nblk - b0 : KNN_I8_MAXBLK;
+            for (int b = 0; b < t.nblk; b++) {
+                t.ptr[b] = blk[b0 + b];
+                t.nc[b] = (int)bnc[b0 + b];
+                t.base[b] = (int64_t)bbase[b0 + b];
+            }
+            RCHK(ctx_step_impl(u, NULL, NULL, 0, 0, &t, s));
+        }
+    } else {
+        RCHK(ctx_step_impl(u, NULL, c->q8, c->step0_nc, c->step0_cbase, NULL, s));
+    }
     /* the sub-search's fail list and count stay on the device: resolve8
      * reads them there, so the only host read is the final count below */
     RCHK(ctx_end_device(u, c->sub_out, s));
@@ -1400,6 +1415,71 @@ static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
     c->fail_list = c->fail_list2;
     c->fail_list2 = t;
     c->nfail = nn;
+    return KNN_OK;
+}
+
+static int research8(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
+{
+    /* INT mode only (c->mode: the device's verdict on the real meta): a
+     * speculative begin (knn_ctx_begin_s8 on a stale host hint) whose data
+     * turned out real-valued fails every query in GEMM mode, and the
+     * sub-search would run GEMM work from a context with no element rows */
+    if (c->mode != KNN_MODE_INT || !c->i8 || c->sub_research || !c->one_block_q8 || c->nstep != 1 || !c->have_hmeta ||
+        c->step0_cbase != c->q_base || c->q_rows_pad != knn_rows_pad(c->block_cap) || c->kp > KNN_KP_M ||
+        env_on("KNN_FORCE_RESCAN") || env_on("KNN_NO_RESEARCH8"))
+        return KNN_OK;
+    return research8_run(c, 0, NULL, NULL, NULL, c->step0_cbase + c->step0_nc, d_out, s);
+}
+
+/* rescan state for c->nfail uncertified queries (knn_ctx_end, and again
+ * after a ring rank's re-search changed the count: the per-query chunk
+ * layout depends on it) */
+static int rescan_prep(knn_ctx_t *c, void *stream)
+{
+    if (c->nfail == 0) return KNN_OK;
+    const size_t need = (size_t)c->nfail * (1 + (size_t)knn_rescan_chunks(c->nfail));
+    if (need > c->rs_cap) {
+        hipFree(c->rs_d);
+        hipFree(c->rs_i);
+        c->rs_d = NULL;
+        c->rs_i = NULL;
+        c->rs_cap = 0;
+        size_t cap = need;
+        if (hipMalloc((void **)&c->rs_d, cap * c->kp * sizeof(double)) != hipSuccess ||
+            hipMalloc((void **)&c->rs_i, cap * c->kp * sizeof(int)) != hipSuccess)
+            return KNN_ERR_NOMEM;
+        c->rs_cap = cap;
+    }
+    return knn_launch_rescan_init(c->kp, c->rs_d, c->rs_i, c->nfail, stream);
+}
+
+/* A ring rank's int8 re-search (include/knn.h): after knn_ctx_end, its
+ * uncertified queries against the byte blocks the rank holds. */
+int knn_ctx_research_blocks(knn_ctx_t *c, int nblk, const void *const *d_sblocks, const size_t *nc,
+                            const size_t *c_base, knn_neighbour_t *d_out, size_t *unresolved, void *stream)
+{
+    if (!c || !d_out || nblk < 1 || !d_sblocks || !nc || !c_base || c->first_step) return KNN_ERR_INVALID;
+    if (unresolved) *unresolved = (size_t)c->nfail;
+    if (c->nfail == 0 || c->mode != KNN_MODE_INT || !c->i8 || c->shadow != 2 || c->sub_research || !c->q8 ||
+        !c->have_hmeta || c->kp > KNN_KP_M || env_on("KNN_FORCE_RESCAN") || env_on("KNN_NO_RESEARCH8"))
+        return KNN_OK;
+    size_t q_end = 0;
+    for (int b = 0; b < nblk; b++) {
+        if (!d_sblocks[b] || nc[b] == 0 || nc[b] > c->block_cap) return KNN_ERR_INVALID;
+        if (c_base[b] + nc[b] > q_end) q_end = c_base[b] + nc[b];
+    }
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int before = c->nfail;
+    const int rc = research8_run(c, nblk, d_sblocks, nc, c_base, q_end, d_out, s);
+    if (rc != KNN_OK) {
+        /* as in knn_ctx_end: the exact rescan resolves the first pass's list */
+        HIPCHK(hipStreamSynchronize(s));
+        (void)hipGetLastError();
+        c->nfail = before;
+    }
+    if (c->nfail != before) RCHK(rescan_prep(c, stream));
+    if (unresolved) *unresolved = (size_t)c->nfail;
     return KNN_OK;
 }
 
@@ -1471,23 +1551,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
         (void)hipGetLastError();
     }
     if (unresolved) *unresolved = (size_t)c->nfail;
-    if (c->nfail > 0) {
-        const size_t need = (size_t)c->nfail * (1 + (size_t)knn_rescan_chunks(c->nfail));
-        if (need > c->rs_cap) {
-            hipFree(c->rs_d);
-            hipFree(c->rs_i);
-            c->rs_d = NULL;
-            c->rs_i = NULL;
-            c->rs_cap = 0;
-            size_t cap = need;
-            if (hipMalloc((void **)&c->rs_d, cap * c->kp * sizeof(double)) != hipSuccess ||
-                hipMalloc((void **)&c->rs_i, cap * c->kp * sizeof(int)) != hipSuccess)
-                return KNN_ERR_NOMEM;
-            c->rs_cap = cap;
-        }
-        RCHK(knn_launch_rescan_init(c->kp, c->rs_d, c->rs_i, c->nfail, stream));
-    }
-    return KNN_OK;
+    return rescan_prep(c, stream);
 }
 
 int knn_ctx_rescan_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base,

@@ -144,6 +144,14 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
 #define KNN_DIST_SHADOW 4  /* with H16: stage the fp16 shadow rows qsh / csh      */
 #define KNN_DIST_SPLIT  8  /* fp32 blocks: split fp16 filter on the split shadow rows
                               qsh / csh (knn_launch_shadow_split); m2s = -2 / S^2   */
+#define KNN_DIST_SPLIT_V1 16 /* with SPLIT: k_dist_topk's 128-row-tile form instead of
+                                k_dist_split (KNN_SPLIT_V1=1; A/B runs)            */
+/* k_dist_split (knn_split.hip): the split fp16 filter on 256-row tiles */
+#define KNN_SPLIT_TC 256
+int knn_launch_dist_split(int dtype, int kl, const void *qsp, const void *qnorm, size_t q_base, int nq,
+                          const void *csp, const void *cnorm, size_t c_base, int nc, size_t c_rows_pad, int n,
+                          const double *meta, int nsplit, double *part_d, int *part_i, double *part_T,
+                          int nq_pad, double *qthr, int uj, int xord, float m2s, void *stream);
 /* fp16 shadow rows (round_up(n, 64) halves a row) of a packed block */
 int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);

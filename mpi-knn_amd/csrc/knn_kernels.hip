@@ -92,37 +92,7 @@ __device__ __forceinline__ knn_h8 knn_to_h8(flt4 a, flt4 b)
     return r;
 }
 
-// ---------------------------------------------------------------------------
-// Mode decision from the max-reduced meta (identical on every rank).
-//   INT : every value an integer and every partial sum of the GEMM form
-//         (norms, dot products, |q|^2+|c|^2, d^2) an integer below 2^p
-//         (p = 53 / 24), so d^2 is exact, bit-identical to the reference's
-//         S, and sqrt is injective on it.  fp64: (2 max|x|)^2 n
-//         <= 2^51; fp32: n max|x|^2 <= 2^23 and n (max - min)^2 <= 2^24.
-//   SCAN: non-finite values or norms near overflow -- no error bound.
-//   GEMM: everything else.
-// ---------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ int knn_mode(const double *meta, int n)
-{
-    if constexpr (sizeof(T) == 8) {
-        if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e290))
-            return KNN_MODE_SCAN;
-        const double lim = 2251799813685248.0 / (4.0 * (double)n);   // 2^51 / 4n
-        double mx = meta[KNN_META_MAXABS];
-        if (meta[KNN_META_NONINT] == 0.0 && mx * mx <= lim) return KNN_MODE_INT;
-        return KNN_MODE_GEMM;
-    } else {
-        if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e37))
-            return KNN_MODE_SCAN;
-        const double mx = meta[KNN_META_MAXABS];
-        const double rg = meta[KNN_META_MAXPOS] + meta[KNN_META_MAXNEG];
-        if (meta[KNN_META_NONINT] == 0.0 && (double)n * mx * mx <= 8388608.0 &&
-            (double)n * rg * rg <= 16777216.0)
-            return KNN_MODE_INT;
-        return KNN_MODE_GEMM;
-    }
-}
+// (knn_mode: the search mode from the reduced meta, knn_device.h)
 
 // Reference-order exact squared distance: S = S + (a-b)^2 over j = 0..n-1,
 // two roundings per feature, no FMA (knn-serial.c:76-85; pow(x,2) -> x*x),
@@ -175,12 +145,12 @@ __device__ __forceinline__ double knn_exact_sq_v(const T *__restrict__ a, const 
 //   2^-22 |q_j c_j| (+ subnormal terms): 3 2^-22 sum|q_j c_j|, 12u qc for d^2.
 //   fp16 products are exact in fp32; each 32-feature chunk's 96 products
 //   are summed apart in fp32 (any order: <= 95u sum|chunk terms|) and the
-//   n/32 chunk sums added to the accumulator (fp32: <= (n/32) u sum|q_j
-//   c_j|; fp64 blocks: fp64, negligible), so d^2 is off by (97 + n/32) 1.01
-//   u qc; norms, qn + cn and the final fma 4u qc.  With a 20% margin (the
-//   MFMA's internal order is not specified; its precision is at least
-//   fp32): ((136 + n/25) u + 4 (n+4) 2^-53) qc (fp64 blocks without the n
-//   term).  Subnormal fp16 halves may be flushed by the MFMA:
+//   n/32 chunk sums added to the fp32 accumulator (<= (n/32) u sum|q_j
+//   c_j|), so d^2 is off by (97 + n/32) 1.01 u qc; norms (fp64 blocks: their
+//   fp64 norms rounded to fp32), qn + cn and the final fma 4u qc.  With a
+//   20% margin (the MFMA's internal order is not specified; its precision
+//   is at least fp32): ((136 + n/25) u + 4 (n+4) 2^-53) qc, fp32 and fp64
+//   blocks alike.  Subnormal fp16 halves may be flushed by the MFMA:
 //   then up to 2^-14 / S <= 2^-27 maxabs is lost per element, the absolute
 //   part 2^-26 maxabs sqrt(n) (|q| + |c|).  The fp32 filter's is ~ (n + 4)
 //   u qc.
@@ -192,8 +162,10 @@ __device__ __forceinline__ double knn_cert_E(int n, double qn, double maxnorm, i
     const double nn = (double)n + 4.0, qc = qn + maxnorm;
     if (split) {
         const double ul = 5.9604644775390625e-08;   // 2^-24
-        // fp32 blocks add the n/32 chunk sums in fp32, fp64 blocks in fp64
-        const double acc = sizeof(TE) == 4 ? (double)n / 25.0 : (double)n * 1e-8;
+        // the n/32 chunk sums are added in fp32 (k_dist_split, fp32 and fp64
+        // blocks alike; k_dist_topk's KNN_SPLIT_V1 form adds fp64 blocks' in
+        // fp64, within this)
+        const double acc = (double)n / 25.0;
         return ((136.0 + acc) * ul + 4.0 * nn * 1.1102230246251565e-16) * qc * (1.0 + 1e-6) +
                1.4901161193847656e-08 * maxabs * sqrt((double)n) * (sqrt(qn) + sqrt(maxnorm));
     }
@@ -2351,6 +2323,9 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
         // split fp16 shadow rows (4 bytes a feature); m2s = -2 / S^2 undoes
         // the scaling in the epilogue's fma (a power of two: exact)
         if (!qsh || !csh) return KNN_ERR_INVALID;
+        if (!(flags & KNN_DIST_SPLIT_V1))
+            return knn_launch_dist_split(dt, KL, qsh, qnorm, q_base, nq, csh, cnorm, c_base, nc, c_rows_pad, n,
+                                         meta, nsplit, part_d, part_i, part_T, nq_pad, qthr, uj, xord, m2s, s);
         const int nps = (int)knn_round_up((size_t)n, 32);
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 3>), grid, dim3(512), 0, s,
                            (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,

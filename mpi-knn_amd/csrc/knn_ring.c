@@ -646,6 +646,23 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         size_t u = 0;
         hipSetDevice(d[g].dev);
         rc = knn_ctx_end(d[g].ctx, d[g].d_out, &u, d[g].cs);
+        if (!rc && u && direct && form && P > 1 && knn_ctx_shadow(d[g].ctx) == 2) {
+            /* the byte blocks of the whole corpus are resident (own + P - 1
+             * received): the int8 re-search of the uncertified queries runs
+             * over them before any element-block exchange */
+            const void *sb[KNN_RING_MAX];
+            size_t snc[KNN_RING_MAX], sbase[KNN_RING_MAX];
+            sb[0] = d[g].qs;
+            snc[0] = d[g].rows;
+            sbase[0] = d[g].base;
+            for (int j = 1; j < P; j++) {
+                const int b = (g - j + P) % P;
+                sb[j] = d[g].rx[j - 1];
+                snc[j] = rows_of(b, R, m);
+                sbase[j] = (size_t)b * R;
+            }
+            rc = knn_ctx_research_blocks(d[g].ctx, P, sb, snc, sbase, d[g].d_out, &u, d[g].cs);
+        }
         unresolved_total += u;
     }
     if (!rc && unresolved_total) {

@@ -253,6 +253,13 @@ class GpuEngine:
     def end(self):
         return self.ctx.end(self.out.data_ptr(), self.stream())
 
+    def research(self, sbufs, rows, bases):
+        """int8 re-search of the queries end() left uncertified against the
+        byte blocks this rank holds (knn_ctx_research_blocks); returns the
+        count still unresolved"""
+        return self.ctx.research_blocks([b.data_ptr() for b in sbufs], rows, bases, self.out.data_ptr(),
+                                        self.stream())
+
     def rescan_end(self):
         self.ctx.rescan_end(self.out.data_ptr(), self.stream())
 
@@ -446,13 +453,25 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
         else:
             for buf, b, r in nz:
                 engine.step(buf, r, b, rescan)
-        return None if use_shadow else fold
+        if use_shadow:
+            # every block of the corpus stays resident in the search's form:
+            # the int8 re-search of uncertified queries runs over them
+            held_s[:] = ([(own, base, rows)] if rows > 0 else []) + [x for x in nz if x[0] is not own]
+            return None
+        return fold
 
+    held_s = []
     if schedule == "direct":
         held = direct_pass(False, None)
     else:
         one_pass(0, False)
     unresolved = engine.end()
+    if (unresolved > 0 and held_s and P > 1 and hasattr(engine, "research") and engine.ctx.shadow() == 2):
+        # a ring rank's uncertified queries: searched again on the int8
+        # contraction (65-entry lists) over the byte blocks it holds, before
+        # any element-block exchange for the exact rescan
+        unresolved = engine.research([x for x, _, _ in held_s], [r for _, _, r in held_s],
+                                     [b for _, b, _ in held_s])
     if verify is not None:
         # (the read-back was enqueued before the search's first kernel, which
         # the merge end() synchronised with waits for: it has landed)

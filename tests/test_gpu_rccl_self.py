@@ -77,7 +77,7 @@ def test_ring_driver_stalled_transfer_times_out(knn, oracle, monkeypatch):
         t0 = time.time()
         with pytest.raises(knn.KnnError) as ei:
             knn.search(X, 30, ngpus=4, layout="col")
-        assert ei.value.args[0] == knn.ERR_RCCL
+        assert ei.value.status == knn.ERR_RCCL
         assert 1.5 < time.time() - t0 < 60
     monkeypatch.delenv("KNN_RING_TEST_STALL")
     got, _ = knn.search(X, 30, ngpus=4, layout="col")

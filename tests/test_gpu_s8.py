@@ -304,3 +304,53 @@ def test_int8_research_every_query_uncertified(knn, oracle, kl, monkeypatch):
         got = e.result()
         assert np.array_equal(got["idx"], ref["idx"]), research
         assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), research
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_int8_research_ring_rank(knn, oracle, P, monkeypatch):
+    """a ring rank's uncertified queries (direct schedule,
+    byte blocks resident) are searched again on the int8 contraction over
+    every byte block the rank holds (knn_ctx_research_blocks) before the
+    element-block exchange of the rescan; clustered data with one corpus
+    split (KNN_SPLITS=1) leaves some uncertified for sure.  Every rank equals
+    the oracle's scan of its rows, with fewer queries left for the rescan
+    than with KNN_NO_RESEARCH8=1."""
+    import torch
+    import mpiknn.ring as ring
+    from test_gpu_ring_rotation import loopback_dist
+    monkeypatch.setenv("KNN_SPLITS", "1")
+    rng = np.random.default_rng(23)
+    base_rows = rng.integers(20, 236, (120, 64)).astype(np.float64)
+    X = np.repeat(base_rows, 25, axis=0) + rng.integers(-2, 3, (3000, 64))
+    X = X[rng.permutation(len(X))]
+    m, n = X.shape
+    dev = torch.device("cuda", 0)
+    Xd = torch.from_numpy(X).to(dev)
+    R, blocks = ring.partition(m, P)
+    counts = {}
+    for mode in ("off", "on"):
+        if mode == "off":
+            monkeypatch.setenv("KNN_NO_RESEARCH8", "1")
+        else:
+            monkeypatch.delenv("KNN_NO_RESEARCH8", raising=False)
+        engines = []
+        for g in range(P):
+            b0, rows = blocks[g]
+            e = ring.GpuEngine(torch, 0, n, R, rows, 30)
+            e.pack(Xd[b0:b0 + rows], layout_col=False, elements=True)
+            engines.append(e)
+        packed = [e.qb.clone() for e in engines]
+        metas = torch.stack([e.meta for e in engines])
+        total = 0
+        for g, e in enumerate(engines):
+            b0, rows = blocks[g]
+            d = loopback_dist(torch, g, P, packed, metas, packed, e, "direct")
+            total += ring.ring_search(d, torch, e, g, P, m, b0, schedule="direct")
+            assert e.ctx.shadow() == 2
+            got = e.result()
+            ref = oracle.knn(X, 30, rows=(b0, rows))
+            assert np.array_equal(got["idx"], ref["idx"]), (mode, P, g)
+            assert np.array_equal(got["distance"].view(np.uint64), ref["distance"].view(np.uint64)), (mode, P, g)
+        counts[mode] = total
+    assert counts["off"] > 0, counts
+    assert counts["on"] < counts["off"], counts

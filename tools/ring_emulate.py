@@ -71,6 +71,8 @@ def main():
                     help="byte-block steps: one launch per block (the neighbour ring), the own "
                          "block then every other block in one launch (the direct-exchange "
                          "ring's default), or all blocks in one launch (KNN_RING_FUSE=all)")
+    ap.add_argument("--no-research", action="store_true",
+                    help="skip the ring rank's int8 re-search of uncertified queries")
     args = ap.parse_args()
 
     import torch
@@ -148,7 +150,13 @@ def main():
                         eng.step_shadow(sbufs[b], rows, base)
                     else:
                         eng.step(bufs[b], rows, base)
-            return eng.end()
+            u = eng.end()
+            u2 = u
+            if u and fuse in ("rest", "all") and not args.no_research:
+                # ring.py's direct schedule: the int8 re-search over the
+                # resident byte blocks before any element-block exchange
+                u2 = eng.research(sbufs, [r for _, r in blocks], [bs for bs, _ in blocks])
+            return u, u2
 
         for _ in range(args.warm):
             one()
@@ -156,9 +164,11 @@ def main():
         # timed without the profiling events (each event record sits on the
         # launch queues), then the same passes profiled for the breakdown
         t0 = time.perf_counter()
-        unres = 0
+        unres = unres2 = 0
         for _ in range(args.steps):
-            unres += one()
+            u, u2 = one()
+            unres += u
+            unres2 += u2
         torch.cuda.synchronize()
         dt_s = (time.perf_counter() - t0) / args.steps
         eng.ctx.profile(1)
@@ -174,7 +184,8 @@ def main():
                   "dist_tflops": flops / (dist_ms * 1e-3) / 1e12 if dist_ms > 0 else None,
                   "exposed_merge_ms_per_pass": merge_ms / args.steps,
                   "splits": eng.ctx.info()[1], "shadow_ring": shadow, "fuse": fuse,
-                  "contraction_bits": eng.ctx.contraction_bits(), "unresolved": unres}
+                  "contraction_bits": eng.ctx.contraction_bits(), "unresolved": unres,
+                  "unresolved_after_research": unres2}
         print(json.dumps({"P": P, **res[P]}), file=sys.stderr, flush=True)
         if sp is not None:
             res["%d/s%d" % (P, sp)] = res.pop(P)
