@@ -339,7 +339,7 @@ static int direct_exchange(ring_dev_t *d, int P, size_t bytes, void *const *send
 /* One direct pass: exchange (form: 0 element blocks, else the shadow form),
  * every device folds its own block, then the P-1 received ones. */
 static int direct_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t n, int dtype, int rescan,
-                       int form, ring_transport_t *t)
+                       int form, ring_transport_t *t, int *aborted)
 {
     void *send[KNN_RING_MAX];
     const void *blk[KNN_RING_MAX];
@@ -360,6 +360,11 @@ static int direct_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t n, int d
         if ((rc = fold_one(&d[g], send[g], d[g].rows, d[g].base, rescan, form))) return rc;
         if ((rc = ring_mark(&d[g], d[g].cs))) return rc;
     }
+    /* the exchange has landed before the steps that read it are enqueued: a
+     * step may synchronise a stream of its own (a growing buffer), which
+     * would block on a transfer that never lands; this wait is bounded (the
+     * own blocks' folds, enqueued above, run meanwhile) */
+    if (P > 1 && (rc = ring_drain(d, P, t, 1, aborted))) return rc;
     for (int g = 0; g < P && P > 1; g++) {
         ring_dev_t *e = &d[g];
         if (hipSetDevice(e->dev) != hipSuccess) return KNN_ERR_HIP;
@@ -407,7 +412,7 @@ static int direct_pass_resident(ring_dev_t *d, int P, size_t R, size_t m)
 /* One full rotation: at step s device g folds block (g - off - s) mod P,
  * where off says how far the blocks have already moved. */
 static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int off,
-                     int rescan, int form, ring_transport_t *t)
+                     int rescan, int form, ring_transport_t *t, int *aborted)
 {
     int rc;
     for (int s = 0; s < P; s++) {
@@ -423,6 +428,10 @@ static int ring_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t bytes, int
                 return KNN_ERR_HIP;
         }
         if (s < P - 1) {
+            /* hop s has landed before step s + 1 is enqueued (bounded; as in
+             * direct_pass: a step's own stream synchronisation must never
+             * wait on a transfer that does not land) */
+            if ((rc = ring_drain(d, P, t, 1, aborted))) return rc;
             for (int g = 0; g < P; g++) {
                 if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
                 if (hipStreamWaitEvent(d[g].cs, d[g].ev_comm, 0) != hipSuccess) return KNN_ERR_HIP;
@@ -635,9 +644,9 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         if (!rc && hipEventRecord(d[g].ev_comp, d[g].cs) != hipSuccess) rc = KNN_ERR_HIP;
     }
     if (!rc && direct)
-        rc = direct_pass(d, P, R, m, n, dtype, 0, form, &tr);
+        rc = direct_pass(d, P, R, m, n, dtype, 0, form, &tr, &aborted);
     else if (!rc)
-        rc = ring_pass(d, P, R, m, form ? knn_ctx_shadow_bytes(d[0].ctx, R) : bytes, 0, 0, form, &tr);
+        rc = ring_pass(d, P, R, m, form ? knn_ctx_shadow_bytes(d[0].ctx, R) : bytes, 0, 0, form, &tr, &aborted);
     /* every transfer of the pass has landed (or the search fails here):
      * knn_ctx_end's synchronisation can then not wait on a stuck hop */
     if (!rc && P > 1) rc = ring_drain(d, P, &tr, 1, &aborted);
@@ -677,7 +686,7 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
         if (!rc && direct) {
             /* element blocks: exchanged again after a shadow-form pass (the
              * receive buffers held shadow blocks), else still resident */
-            rc = form ? direct_pass(d, P, R, m, n, dtype, 1, 0, &tr)
+            rc = form ? direct_pass(d, P, R, m, n, dtype, 1, 0, &tr, &aborted)
                       : direct_pass_resident(d, P, R, m);
         } else if (!rc && form) {
             /* the pass moved shadow blocks: a fresh rotation of element blocks */
@@ -685,9 +694,9 @@ int knn_search_ring_host(const double *X, size_t m, size_t n, int layout, int k,
                 d[g].cur = d[g].qb;
                 d[g].nxt = d[g].rx[++d[g].hop % NRX];
             }
-            rc = ring_pass(d, P, R, m, bytes, 0, 1, 0, &tr);
+            rc = ring_pass(d, P, R, m, bytes, 0, 1, 0, &tr, &aborted);
         } else if (!rc) {
-            rc = ring_pass(d, P, R, m, bytes, P - 1, 1, 0, &tr);
+            rc = ring_pass(d, P, R, m, bytes, P - 1, 1, 0, &tr, &aborted);
         }
         if (!rc && P > 1) rc = ring_drain(d, P, &tr, 1, &aborted);
         for (int g = 0; g < P && !rc; g++) {
