@@ -26,6 +26,7 @@ N > 1: one process per GPU, RCCL (torch.distributed "nccl") ring of corpus
 blocks, strong scaling (total work fixed).  Rank 0 prints one JSON line.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -240,18 +241,36 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
     # per rank per step, over its measured event time
     flops_rank = 2.0 * rows * m * n * prof_steps
     achieved = flops_rank / (dist_ms * 1e-3) / 1e12 if dist_ms > 0 else None
-    traffic = None
+    # the MFMA the contraction ran on: fp32 searches on exactly representable
+    # 8-bit-style integer data contract on fp16 MFMA (include/knn.h)
+    split = engine.ctx.split()
+    kernel = "k_dist_topk_i8" if cbits == 8 else ("k_dist_split" if split and
+                                                  os.environ.get("KNN_SPLIT_V1", "0") != "1" else "k_dist_topk")
+    traffic, traffic_src, traffic_stale = None, None, None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
         key = "m%d_n%d_p%d" % (m, n, P) + ("" if dtype == "f64" else "_" + dtype) + \
             ("_real" if workload == "mnist-real" else "")
-        traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+        rec = tj.get(key)
+        if rec:
+            # the PMC figure counts only while it was taken on the kernel that
+            # runs here, built from the source as it is now
+            src = rec.get("source")
+            same = (str(rec.get("kernel", "")).split("<")[0] == kernel and src is not None and
+                    os.path.exists(os.path.join(ROOT, src)) and
+                    hashlib.sha1(open(os.path.join(ROOT, src), "rb").read()).hexdigest() == rec.get("source_sha1"))
+            if same:
+                traffic = rec.get("hbm_bytes_per_launch")
+                traffic_src = ("rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE of %s on the same workload at P = 1 "
+                               "(%s; kernel source sha1 %s = this build's; not measured inside this run)"
+                               % (rec["kernel"], rec.get("profile", "profiles/pmc_traffic.json"),
+                                  rec["source_sha1"][:12]))
+            else:
+                traffic_stale = ("profiles/pmc_traffic.json[%s] was measured on %s built from an older source "
+                                 "(%s); not reported" % (key, rec.get("kernel"), rec.get("profile", "?")))
+    except (OSError, ValueError, KeyError, TypeError):
         pass
-    # the MFMA the contraction ran on: fp32 searches on exactly representable
-    # 8-bit-style integer data contract on fp16 MFMA (include/knn.h)
-    split = engine.ctx.split()
     peak = {64: FP64_MFMA_PEAK_TFLOPS, 32: FP32_MFMA_PEAK_TFLOPS,
             16: FP16_MFMA_PEAK_TFLOPS, 8: I8_MFMA_PEAK_TOPS}[cbits]
     if split:
@@ -260,7 +279,7 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         peak = FP16_MFMA_PEAK_TFLOPS / 3.0
     dtype_peak = FP64_MFMA_PEAK_TFLOPS if dtype == "f64" else FP32_MFMA_PEAK_TFLOPS
     roofline = {
-        "kernel": "k_dist_topk_i8" if cbits == 8 else "k_dist_topk",
+        "kernel": kernel,
         "bound": "mfma",
         "achieved": achieved,
         "peak": peak,
@@ -281,8 +300,8 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         "dtype_peak_equiv": (achieved / dtype_peak) if (achieved and cbits < 32) else None,
         "filter": "split-f16" if split else None,
         "traffic": traffic,
-        "traffic_source": "rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE of the same workload at P = 1 "
-                          "(profiles/pmc_traffic.json; not measured inside this run)" if traffic else None,
+        "traffic_source": traffic_src,
+        "traffic_stale": traffic_stale,
         # distance-stage busy time (union of the overlapped k_dist_topk
         # launches, knn_ctx_profile) per launch; at P = 1 one launch a step
         "avg_launch_ms": dist_ms / max(launches, 1),

@@ -341,10 +341,15 @@ def test_int8_research_ring_rank(knn, oracle, P, monkeypatch):
             engines.append(e)
         packed = [e.qb.clone() for e in engines]
         metas = torch.stack([e.meta for e in engines])
+        wires = []
+        for e in engines:
+            w = torch.empty(knn.wire_bytes(R, n), dtype=torch.uint8, device=dev)
+            knn.wire_pack(w.data_ptr(), e.qb.data_ptr(), R, n, "f64", e.stream())
+            wires.append(w)
         total = 0
         for g, e in enumerate(engines):
             b0, rows = blocks[g]
-            d = loopback_dist(torch, g, P, packed, metas, packed, e, "direct")
+            d = loopback_dist(torch, g, P, packed, metas, wires, e, "direct")
             total += ring.ring_search(d, torch, e, g, P, m, b0, schedule="direct")
             assert e.ctx.shadow() == 2
             got = e.result()

@@ -40,8 +40,30 @@ def per_launch(pass_dir):
     return {k: {c: v / len(disp[k]) for c, v in cs.items()} for k, cs in tot.items()}
 
 
+DIST_KERNELS = ("k_dist_topk", "k_dist_split")
+# the source each distance kernel is built from: the PMC record carries its
+# sha1, and bench.py reports the traffic only while the source is unchanged
+KERNEL_SOURCES = (("k_dist_topk_i8", "mpi-knn_amd/csrc/knn_i8.hip"),
+                  ("k_dist_split", "mpi-knn_amd/csrc/knn_split.hip"),
+                  ("k_dist_topk", "mpi-knn_amd/csrc/knn_kernels.hip"))
+
+
+def kernel_source(kname):
+    for pre, path in KERNEL_SOURCES:
+        if kname and kname.startswith(pre):
+            return path
+    return None
+
+
+def sha1_of(path):
+    import hashlib
+    return hashlib.sha1(open(os.path.join(ROOT, path), "rb").read()).hexdigest()
+
+
 def dominant(d):
-    ks = [k for k in d if k.startswith("k_dist_topk")]
+    """the distance kernel with the most dispatches' worth of counters (the
+    search's own instantiation, not the int8 re-search's)"""
+    ks = [k for k in d if k.startswith(DIST_KERNELS)]
     return ks[0] if ks else None
 
 
@@ -57,7 +79,7 @@ def steady(trace_dir, bench_line):
     for f in fs:
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-            if k.startswith("k_dist_topk"):
+            if k.startswith(DIST_KERNELS):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k))
     if not rows:
         return None
@@ -131,7 +153,10 @@ def main():
     rec = None
     if fetch and write:
         f, w = statistics.median(fetch), statistics.median(write)
-        rec = {"kernel": kname, "fetch_bytes": f, "write_bytes": w, "hbm_bytes_per_launch": f + w,
+        src = kernel_source(kname)
+        rec = {"kernel": kname, "source": src, "source_sha1": sha1_of(src) if src else None,
+               "profile": "profiles/%s_%s_summary.md" % (TAG, WL),
+               "fetch_bytes": f, "write_bytes": w, "hbm_bytes_per_launch": f + w,
                "samples_fetch_bytes": fetch, "samples_write_bytes": write,
                "algorithmic_bytes_per_launch": m * n * es,
                "note": "median of %d passes; FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KiB->B, one launch = "
