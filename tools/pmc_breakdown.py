@@ -27,7 +27,7 @@ def main():
     res = {}
     for d in sys.argv[1:]:
         for (k, disp), cs in sorted(per_dispatch(d).items()):
-            if not k.startswith(("k_dist_topk", "k_merge")):
+            if not k.startswith(("k_dist_topk", "k_dist_split", "k_merge")):
                 continue
             rec = dict(cs)
             w = cs.get("SQ_WAVES")
