@@ -416,7 +416,7 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     c->kl = knn_kl_for(c->kp, dtype);
     c->lpq = 4;
     c->klx = c->kl;
-    c->xord = env_on("KNN_XCD_ORDER");   /* split-major by default (the XCD-grouped order measured no faster) */
+    c->xord = getenv("KNN_XCD_ORDER") && getenv("KNN_XCD_ORDER")[0] == '1';   /* split-major by default (the XCD-grouped order measured no faster) */
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
 
     const size_t np = c->nq_pad;
