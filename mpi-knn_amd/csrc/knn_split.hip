@@ -52,6 +52,22 @@ typedef _Float16 knn_sh8 __attribute__((ext_vector_type(8)));
 #define SP_NORM_OFF (SP_NST * SP_STAGE)       /* 147456 */
 #define SP_NORM_SLOT 2048                     /* 256 norms x 8 B (fp32: first 1 KiB) */
 #define SP_LDS (SP_NORM_OFF + 4 * SP_NORM_SLOT)
+// Diagnostic builds only (tools/split_ablate.sh compiles copies with one of
+// these set; the product library is built with none): SP_ABL_NOEPI skips the
+// epilogue, SP_ABL_NOMFMA the contraction, SP_ABL_NOFRAG the fragment reads,
+// SP_ABL_NODMA the staging loads.
+#ifndef SP_ABL_NOEPI
+#define SP_ABL_NOEPI 0
+#endif
+#ifndef SP_ABL_NOMFMA
+#define SP_ABL_NOMFMA 0
+#endif
+#ifndef SP_ABL_NOFRAG
+#define SP_ABL_NOFRAG 0
+#endif
+#ifndef SP_ABL_NODMA
+#define SP_ABL_NODMA 0
+#endif
 
 // fp64 bound -> fp32 bound rounded up (still a bound: a candidate above it
 // is above the fp64 one)
@@ -126,6 +142,7 @@ __global__ __launch_bounds__(512) void k_dist_split(
     // query rows 16 w + 8 (i - 4)..; rows past the block's allocation are
     // clamped to its last row (their candidates are masked by index)
     auto glds1 = [&](int i) {
+        if (SP_ABL_NODMA) return;
         const unsigned dst0 = (unsigned)(uintptr_t)lds + (unsigned)s_st * SP_STAGE;
         if (i < 4) {
             const char *cb = csp + (size_t)s_t * SP_TC * rsb + (size_t)128 * s_fc;
@@ -169,6 +186,13 @@ __global__ __launch_bounds__(512) void k_dist_split(
 
     // ---- epilogue of tile t: d^2, threshold filter, insertion ------------
     auto epilogue = [&](int t) {
+        if (SP_ABL_NOEPI) {
+#pragma unroll
+            for (int mt = 0; mt < 16; mt++) asm volatile("" ::"v"(acc[mt]));
+#pragma unroll
+            for (int mt = 0; mt < 16; mt++) acc[mt] = (flt4){0, 0, 0, 0};
+            return;
+        }
         const LDS_AS T *cng = (const LDS_AS T *)(lds + SP_NORM_OFF + (t & 3) * SP_NORM_SLOT) + 64 * g;
         const float lim = L[KL - 1] < thr ? L[KL - 1] : thr;
         const int row0 = t * SP_TC;
@@ -274,15 +298,19 @@ __global__ __launch_bounds__(512) void k_dist_split(
             gnorm(t + 2);
             for (int fc = 0; fc < nfc; fc++) {
                 LDS_AS char *cs = lds + st * SP_STAGE;
-                const knn_sh8 qh = *(const LDS_AS knn_sh8 *)(cs + SP_QOFF + wave_s * 2048 + fs0);
-                const knn_sh8 ql = *(const LDS_AS knn_sh8 *)(cs + SP_QOFF + wave_s * 2048 + fs1);
-                knn_sh8 ah[2], al[2];
-                ah[0] = *(const LDS_AS knn_sh8 *)(cs + fs0);
-                al[0] = *(const LDS_AS knn_sh8 *)(cs + fs1);
+                knn_sh8 qh, ql, ah[2], al[2];
+                if (SP_ABL_NOFRAG) {
+                    qh = ql = ah[0] = al[0] = ah[1] = al[1] = (knn_sh8){1, 0, 0, 0, 0, 0, 0, 0};
+                } else {
+                    qh = *(const LDS_AS knn_sh8 *)(cs + SP_QOFF + wave_s * 2048 + fs0);
+                    ql = *(const LDS_AS knn_sh8 *)(cs + SP_QOFF + wave_s * 2048 + fs1);
+                    ah[0] = *(const LDS_AS knn_sh8 *)(cs + fs0);
+                    al[0] = *(const LDS_AS knn_sh8 *)(cs + fs1);
+                }
                 flt4 tt[2];
 #pragma unroll
                 for (int mt = 0; mt < 16; mt++) {
-                    if (mt + 1 < 16) {
+                    if (mt + 1 < 16 && !SP_ABL_NOFRAG) {
                         ah[(mt + 1) & 1] = *(const LDS_AS knn_sh8 *)(cs + (mt + 1) * 2048 + fs0);
                         al[(mt + 1) & 1] = *(const LDS_AS knn_sh8 *)(cs + (mt + 1) * 2048 + fs1);
                     }
@@ -295,9 +323,14 @@ __global__ __launch_bounds__(512) void k_dist_split(
                     }
                     // the chunk's 96 products summed apart (cross terms
                     // first), then added to the accumulator (knn_cert_E)
-                    flt4 x = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mt & 1], ql, (flt4){0, 0, 0, 0}, 0, 0, 0);
-                    x = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mt & 1], qh, x, 0, 0, 0);
-                    tt[mt & 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mt & 1], qh, x, 0, 0, 0);
+                    if (SP_ABL_NOMFMA) {
+                        asm volatile("" ::"v"(ah[mt & 1]), "v"(al[mt & 1]), "v"(qh), "v"(ql));
+                        tt[mt & 1] = (flt4){0, 0, 0, 0};
+                    } else {
+                        flt4 x = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mt & 1], ql, (flt4){0, 0, 0, 0}, 0, 0, 0);
+                        x = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mt & 1], qh, x, 0, 0, 0);
+                        tt[mt & 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mt & 1], qh, x, 0, 0, 0);
+                    }
                     if (mt > 0) acc[mt - 1] += tt[(mt - 1) & 1];
                     __builtin_amdgcn_sched_barrier(0);
                 }
