@@ -623,7 +623,7 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
      * query); KNN_I8_W8=1 keeps the 8-wave kernel on 128-row tiles (4) */
     c->lpq = c->i8 ? (c->sub_research ? 2 : (c->klx == KNN_I8_KL_S && env_on("KNN_I8_W8") ? 4 : knn_i8_lpq(c->kp, c->klx)))
                    : 4;
-    c->i8_wgpc = c->i8 && c->klx == KNN_I8_KL_S && c->lpq == 2 && !knn_i8_qg2l(c->n) ? 2 : 1;
+    c->i8_wgpc = c->i8 && c->klx == KNN_I8_KL_S && c->lpq == 2 ? 2 : 1;
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
      * element fragments in the kernel instead) */
     c->shadow = c->i8 ? 2 : (c->h16 && !env_on("KNN_NO_SHADOW"));
@@ -840,9 +840,7 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
          * ring's fused launch keeps 3: at P = 8 4 splits left 192 a pass
          * for the rescan, 5 splits 27) */
         const int kl = c->klx;
-        /* (the half-tile lane layout: 2 lists a query over 64-row tiles) */
-        const int half = c->klx == KNN_I8_KL_S && c->lpq == 2;
-        const int f2 = (half && knn_s8_rs(c->n) / 32 > 8)
+        const int f2 = (c->i8_wgpc == 2 && knn_s8_rs(c->n) / 32 > 8)
                            ? 10
                            : (c->split_solo && knn_i8_qg(c->klx, c->lpq, c->n) == 2 ? 5 : 6);
         s_min = (f2 * (c->k + 1) + 2 * c->lpq * kl - 1) / (2 * c->lpq * kl);
@@ -864,7 +862,7 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
      * work and a set of cold lists.  A single round (a ring rank's fused
      * launch) still takes the model: P = 8 6 / 7 / 8 splits 0.75 / 0.69 /
      * 0.67 ms a rank, the model's 8 */
-    if (c->i8 && c->klx == KNN_I8_KL_S && c->lpq == 2 && !short_rows && nqb * s_min >= slots) {
+    if (c->i8 && c->i8_wgpc == 2 && !short_rows && nqb * s_min >= slots) {
         best = s_min;
         /* between one and two rounds at s_min (a P = 4 rank's launches:
          * 118 query blocks x 7 splits on 512 slots), one full round wins

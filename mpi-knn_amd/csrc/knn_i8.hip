@@ -292,8 +292,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     constexpr int TB0 = XB0 + (RHN == 2 ? 3 * 8 * 32 * 4 : 0);   // block table
     static_assert(MB == 2 || MB == 4, "m-blocks a wave");
     static_assert(PW == 2 || PW == 4, "DMA pieces a wave");
-    static_assert(QG == 1 || (QG == 2 && RHN == 1 && (NKS <= 8 || WPS == 1)),
-                  "two query groups: 4-wave kernels, short rows or one wave a SIMD");
+    static_assert(QG == 1 || (QG == 2 && RHN == 1 && NKS <= 8), "two query groups: 4-wave short-row kernels");
     constexpr int QB = 128 * QG;            // queries a workgroup
     // rows of <= 4 K-steps carry init words (K2 / IW form); longer rows the
     // whole norm in the slot word and zero init words (knn_device.h): their
@@ -517,8 +516,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // their L[S8] / L[S16])
     constexpr bool REREAD = KL != KNN_I8_KL_L;
     // (QG = 2: no summaries -- their 8 VGPRs a group spill there)
-    // (one wave a SIMD: 512 registers, room for both groups' summaries)
-    constexpr bool SUM = REREAD && KL == KNN_I8_KL_S && (QG == 1 || WPS == 1);
+    constexpr bool SUM = REREAD && KL == KNN_I8_KL_S && QG == 1;
     constexpr int S8 = 8 / LPQ - 1, S16 = 16 / LPQ - 1;
     int q_pubx[QG];
 #pragma unroll
@@ -1060,11 +1058,6 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int lpq, int k, const void *qs
         // Rows of <= 4 K-steps (SIFT): two query groups a wave, a 7-stage
         // ring (the second group's survivor buffers take the 8th stage's LDS)
         if (nks <= 4 && qg == 2) launch_i8<KNN_I8_KL_S, 4, 4, 2, 7, 5, 2, 2>(I8_ARGS);
-        // long rows, two groups a wave at one wave a SIMD (KNN_I8_QG2L=1):
-        // one 256-query workgroup a CU, a 12-stage ring in the LDS it frees
-        else if (qg == 2 && nks <= 16) launch_i8<KNN_I8_KL_S, 16, 4, 1, 12, 5, 2, 2>(I8_ARGS);
-        else if (qg == 2 && nks <= 25) launch_i8<KNN_I8_KL_S, 25, 4, 1, 12, 5, 2, 2>(I8_ARGS);
-        else if (qg == 2) launch_i8<KNN_I8_KL_S, 28, 4, 1, 12, 5, 2, 2>(I8_ARGS);
         else if (nks <= 4) launch_i8<KNN_I8_KL_S, 4, 4, 2, 8, 5, 2>(I8_ARGS);
         else if (nks <= 8) launch_i8<KNN_I8_KL_S, 8, 4, 2, 8, 5, 2>(I8_ARGS);
         else if (nks <= 16) launch_i8<KNN_I8_KL_S, 16, 4, 2, 8, 5, 2>(I8_ARGS);

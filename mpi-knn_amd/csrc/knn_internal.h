@@ -114,15 +114,6 @@ static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL_S : KNN_
  * lists on 64-row half tiles (the k <= 32 default); 4 for the 8-wave
  * kernel on 128-row tiles (17-entry lists, or KNN_I8_W8=1) */
 static inline int knn_i8_lpq(int kp, int kl) { return kp <= KNN_KP_M && kl != KNN_I8_KL_S ? 4 : 2; }
-/* long rows (> 4 K-steps: MNIST) on the one-wave-a-SIMD form of the
- * half-tile kernel (KNN_I8_QG2L=1): two query groups a wave share every A
- * fragment, 512 registers a wave hold both groups' query fragments, one
- * workgroup of 256 queries a CU */
-static inline int knn_i8_qg2l(size_t n)
-{
-    const char *e = getenv("KNN_I8_QG2L");
-    return knn_s8_rs(n) / 32 > 4 && knn_s8_rs(n) / 32 <= 28 && e && *e == '1';
-}
 /* query groups a wave of the int8 kernel: 2 for the half-tile kernel on
  * rows of <= 4 K-steps (SIFT's n = 128: a workgroup of 256 queries, A
  * fragments and init words shared by both groups), else 1
@@ -130,8 +121,7 @@ static inline int knn_i8_qg2l(size_t n)
 static inline int knn_i8_qg(int kl, int lpq, size_t n)
 {
     const char *e = getenv("KNN_I8_QG1");
-    if (kl != KNN_I8_KL_S || lpq != 2 || (e && *e && *e != '0')) return 1;
-    return knn_s8_rs(n) / 32 <= 4 || knn_i8_qg2l(n) ? 2 : 1;
+    return kl == KNN_I8_KL_S && lpq == 2 && knn_s8_rs(n) / 32 <= 4 && !(e && *e && *e != '0') ? 2 : 1;
 }
 static inline size_t knn_n_pad_dt(size_t n, int dtype)
 {

@@ -46,10 +46,9 @@ typedef _Float16 knn_sh8 __attribute__((ext_vector_type(8)));
 
 #define SP_TQ 128
 #define SP_TC 256
-#define SP_NST 3
-#define SP_STAGE 49152                        /* 32 KiB corpus + 16 KiB queries */
-#define SP_QOFF 32768
-#define SP_NORM_OFF (SP_NST * SP_STAGE)       /* 147456 */
+#define SP_NST 4
+#define SP_STAGE 32768                        /* 256 corpus rows x 128 B */
+#define SP_NORM_OFF (SP_NST * SP_STAGE)       /* 131072 */
 #define SP_NORM_SLOT 2048                     /* 256 norms x 8 B (fp32: first 1 KiB) */
 #define SP_LDS (SP_NORM_OFF + 4 * SP_NORM_SLOT)
 // Diagnostic builds only (tools/split_ablate.sh compiles copies with one of
@@ -78,7 +77,11 @@ __device__ __forceinline__ float sp_bound_up(double d)
     return f;
 }
 
-template <typename T, int KL>
+typedef int knn_si4 __attribute__((ext_vector_type(4)));
+
+// D: A-fragment prefetch depth in m-tiles (the ds_reads of m-tile mt + D
+// issue right after m-tile mt's MFMAs)
+template <typename T, int KL, int D>
 __global__ __launch_bounds__(512) void k_dist_split(
     const char *__restrict__ qsp, const T *__restrict__ qnorm, size_t q_base, int nq,
     const char *__restrict__ csp, const T *__restrict__ cnorm, size_t c_base, int nc, int c_rows_lim,
@@ -138,24 +141,18 @@ __global__ __launch_bounds__(512) void k_dist_split(
     const int lr = lane >> 3, ls = lane & 7;
     const int seg_b = 16 * (ls ^ lr);
     int s_c = 0, s_t = t_lo, s_fc = 0, s_st = 0;      // chunk being staged, its stage
-    // piece i of the chunk: 0..3 corpus rows 32 w + 8 i.. of the tile, 4..5
-    // query rows 16 w + 8 (i - 4)..; rows past the block's allocation are
-    // clamped to its last row (their candidates are masked by index)
+    // piece i (0..3) of a chunk: corpus rows 32 w + 8 i.. of the tile; rows
+    // past the block's allocation are clamped to its last row (their
+    // candidates are masked by index)
     auto glds1 = [&](int i) {
         if (SP_ABL_NODMA) return;
         const unsigned dst0 = (unsigned)(uintptr_t)lds + (unsigned)s_st * SP_STAGE;
-        if (i < 4) {
-            const char *cb = csp + (size_t)s_t * SP_TC * rsb + (size_t)128 * s_fc;
-            const int lim = c_rows_lim - 1 - s_t * SP_TC;
-            int lrow = 32 * wave_s + 8 * i + lr;
-            lrow = lrow < lim ? lrow : lim;
-            bglds16(knn_rsrc(cb), (unsigned)(lrow * rsb + seg_b),
-                    dst0 + (unsigned)(2 * wave_s + (i >> 1)) * 2048u + (unsigned)(i & 1) * 1024u);
-        } else {
-            const char *qb0 = qsp + (size_t)qrow0 * rsb + (size_t)128 * s_fc;
-            bglds16(knn_rsrc(qb0), (unsigned)((16 * wave_s + 8 * (i - 4) + lr) * rsb + seg_b),
-                    dst0 + SP_QOFF + (unsigned)wave_s * 2048u + (unsigned)(i - 4) * 1024u);
-        }
+        const char *cb = csp + (size_t)s_t * SP_TC * rsb + (size_t)128 * s_fc;
+        const int lim = c_rows_lim - 1 - s_t * SP_TC;
+        int lrow = 32 * wave_s + 8 * i + lr;
+        lrow = lrow < lim ? lrow : lim;
+        bglds16(knn_rsrc(cb), (unsigned)(lrow * rsb + seg_b),
+                dst0 + (unsigned)(2 * wave_s + (i >> 1)) * 2048u + (unsigned)(i & 1) * 1024u);
     };
     auto advance = [&]() {
         s_c++;
@@ -166,6 +163,18 @@ __global__ __launch_bounds__(512) void k_dist_split(
                 s_t++;
             }
         }
+    };
+    // The query fragments (B) of a chunk straight into registers: a lane's
+    // two 16-byte slots (hi g, lo 4 + g) of its query row -- the only wave
+    // that reads them, so no LDS round trip.  Issued from asm one chunk
+    // ahead (counted by the ring's vmcnt waits, invisible to the compiler's
+    // wait pass, which would otherwise drain the LDS-DMA ring before their
+    // first use) and laundered after the wait that saw them land.
+    const char *qrow = qsp + (size_t)myq * rsb + 16 * g;
+    auto bload = [&](int fc, knn_si4 &h, knn_si4 &l) {
+        const char *p = qrow + (size_t)128 * fc;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(h) : "v"(p) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(l) : "v"(p) : "memory");
     };
     // norm slice of tile t (clamped to the split) into ring slot t & 3:
     // [g][mt][r] = norm of tile row 16 mt + 4 g + r, in 4-byte pieces
@@ -280,64 +289,81 @@ __global__ __launch_bounds__(512) void k_dist_split(
     const int fs1 = j16 * 128 + 16 * ((4 + g) ^ (j16 & 7));    // slot 4 + g: lo halves
 
     if (total > 0) {
-        // prologue: norm slices of the first two tiles, chunks 0 and 1
+        // prologue: chunk 0's query fragments, the norm slices of the first
+        // two tiles, chunks 0..2 (chunk 3 is staged during chunk 0)
+        knn_si4 qh_c, ql_c, qh_n, ql_n;
+        bload(0, qh_c, ql_c);
         gnorm(t_lo);
         gnorm(t_lo + 1);
 #pragma unroll
-        for (int x = 0; x < 2; x++) {
+        for (int x = 0; x < SP_NST - 1; x++) {
 #pragma unroll
-            for (int i = 0; i < 6; i++) glds1(i);
+            for (int i = 0; i < 4; i++) glds1(i);
             advance();
         }
-        // norms + chunk 0 landed (chunk 1's 6 pieces may stay in flight)
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        // B(0), norms, chunk 0 landed: chunks 1, 2 (8 pieces) may stay in flight
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        asm volatile("" : "+v"(qh_c), "+v"(ql_c));
         __builtin_amdgcn_s_barrier();
 
-        int st = 0;                                   // stage of the chunk computed
+        int st = 0, fcq = 0;                          // stage / row chunk computed
         for (int t = t_lo; t < t_hi; t++) {
             gnorm(t + 2);
             for (int fc = 0; fc < nfc; fc++) {
                 LDS_AS char *cs = lds + st * SP_STAGE;
-                knn_sh8 qh, ql, ah[2], al[2];
+                // next chunk's query fragments (the row's chunks cycle every tile)
+                fcq = fcq + 1 == nfc ? 0 : fcq + 1;
+                bload(fcq, qh_n, ql_n);
+                knn_sh8 qh, ql, ah[D], al[D];
                 if (SP_ABL_NOFRAG) {
-                    qh = ql = ah[0] = al[0] = ah[1] = al[1] = (knn_sh8){1, 0, 0, 0, 0, 0, 0, 0};
+                    qh = ql = (knn_sh8){1, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                    for (int d = 0; d < D; d++) ah[d] = al[d] = qh;
                 } else {
-                    qh = *(const LDS_AS knn_sh8 *)(cs + SP_QOFF + wave_s * 2048 + fs0);
-                    ql = *(const LDS_AS knn_sh8 *)(cs + SP_QOFF + wave_s * 2048 + fs1);
-                    ah[0] = *(const LDS_AS knn_sh8 *)(cs + fs0);
-                    al[0] = *(const LDS_AS knn_sh8 *)(cs + fs1);
+                    qh = __builtin_bit_cast(knn_sh8, qh_c);
+                    ql = __builtin_bit_cast(knn_sh8, ql_c);
+#pragma unroll
+                    for (int d = 0; d < D; d++) {
+                        ah[d] = *(const LDS_AS knn_sh8 *)(cs + d * 2048 + fs0);
+                        al[d] = *(const LDS_AS knn_sh8 *)(cs + d * 2048 + fs1);
+                    }
                 }
                 flt4 tt[2];
 #pragma unroll
                 for (int mt = 0; mt < 16; mt++) {
-                    if (mt + 1 < 16 && !SP_ABL_NOFRAG) {
-                        ah[(mt + 1) & 1] = *(const LDS_AS knn_sh8 *)(cs + (mt + 1) * 2048 + fs0);
-                        al[(mt + 1) & 1] = *(const LDS_AS knn_sh8 *)(cs + (mt + 1) * 2048 + fs1);
-                    }
-                    // chunk c + 2 into the stage chunk c - 1 left (freed by
-                    // the barrier that ended chunk c - 1), one piece every
-                    // second m-tile
-                    if ((mt & 1) && mt < 12) {
-                        glds1(mt >> 1);
-                        if (mt == 11) advance();
-                    }
+                    const int sl = mt % D;
                     // the chunk's 96 products summed apart (cross terms
                     // first), then added to the accumulator (knn_cert_E)
                     if (SP_ABL_NOMFMA) {
-                        asm volatile("" ::"v"(ah[mt & 1]), "v"(al[mt & 1]), "v"(qh), "v"(ql));
+                        asm volatile("" ::"v"(ah[sl]), "v"(al[sl]), "v"(qh), "v"(ql));
                         tt[mt & 1] = (flt4){0, 0, 0, 0};
                     } else {
-                        flt4 x = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mt & 1], ql, (flt4){0, 0, 0, 0}, 0, 0, 0);
-                        x = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mt & 1], qh, x, 0, 0, 0);
-                        tt[mt & 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mt & 1], qh, x, 0, 0, 0);
+                        flt4 x = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[sl], ql, (flt4){0, 0, 0, 0}, 0, 0, 0);
+                        x = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[sl], qh, x, 0, 0, 0);
+                        tt[mt & 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[sl], qh, x, 0, 0, 0);
+                    }
+                    // m-tile mt + D's fragments into the slot just consumed
+                    if (mt + D < 16 && !SP_ABL_NOFRAG) {
+                        ah[sl] = *(const LDS_AS knn_sh8 *)(cs + (mt + D) * 2048 + fs0);
+                        al[sl] = *(const LDS_AS knn_sh8 *)(cs + (mt + D) * 2048 + fs1);
                     }
                     if (mt > 0) acc[mt - 1] += tt[(mt - 1) & 1];
+                    // chunk c + 3 into the stage chunk c - 1 left (freed by the
+                    // barrier that ended chunk c - 1), one piece every 4th m-tile
+                    if ((mt & 3) == 2) {
+                        glds1(mt >> 2);
+                        if (mt == 14) advance();
+                    }
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 acc[15] += tt[1];
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this stage's reads done
-                // chunk c + 1 landed: chunk c + 2's 6 pieces may stay in flight
-                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                // the next chunk's query fragments and pieces landed (and
+                // chunk c + 2's): chunk c + 3's 4 pieces may stay in flight
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                asm volatile("" : "+v"(qh_n), "+v"(ql_n));
+                qh_c = qh_n;
+                ql_c = ql_n;
                 __builtin_amdgcn_s_barrier();
                 st = st == SP_NST - 1 ? 0 : st + 1;
             }
@@ -366,7 +392,7 @@ __global__ __launch_bounds__(512) void k_dist_split(
     }
 }
 
-template <typename T, int KL>
+template <typename T, int KL, int D>
 static int launch_split(const void *qsp, const T *qnorm, size_t q_base, int nq, const void *csp,
                         const T *cnorm, size_t c_base, int nc, size_t c_rows_pad, int n, const double *meta,
                         int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad, double *qthr, int uj,
@@ -376,7 +402,7 @@ static int launch_split(const void *qsp, const T *qnorm, size_t q_base, int nq, 
     const int nqb = (nq + SP_TQ - 1) / SP_TQ;
     const int ntiles = (nc + SP_TC - 1) / SP_TC;
     const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_split<T, KL>), dim3((unsigned)(nqb_grid * nsplit)), dim3(512), 0, s,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_split<T, KL, D>), dim3((unsigned)(nqb_grid * nsplit)), dim3(512), 0, s,
                        (const char *)qsp, qnorm, q_base, nq, (const char *)csp, cnorm, c_base, nc,
                        (int)c_rows_pad, n, rsb, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
                        (unsigned long long *)qthr, uj, xord, m2s);
@@ -397,7 +423,7 @@ extern "C" int knn_launch_dist_split(int dtype, int kl, const void *qsp, const v
     if ((nc + SP_TC - 1) / SP_TC < nsplit) return KNN_ERR_INVALID;
     hipStream_t s = (hipStream_t)stream;
 #define SPL(T, KL)                                                                                         \
-    return launch_split<T, KL>(qsp, (const T *)qnorm, q_base, nq, csp, (const T *)cnorm, c_base, nc, c_rows_pad, \
+    return launch_split<T, KL, (KL > 24 ? 2 : 4)>(qsp, (const T *)qnorm, q_base, nq, csp, (const T *)cnorm, c_base, nc, c_rows_pad, \
                                n, meta, nsplit, part_d, part_i, part_T, nq_pad, qthr, uj, xord, m2s, s)
     if (dtype == KNN_F64 && kl == KNN_KL) SPL(double, KNN_KL);
     if (dtype == KNN_F32 && kl == KNN_KL) SPL(float, KNN_KL);
