@@ -338,6 +338,13 @@ KNN_API int knn_ctx_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
  * byte blocks with KNN_NO_FUSE=1). */
 KNN_API int knn_ctx_step_shadow_n(knn_ctx_t *ctx, int nblk, const void *const *d_sblocks,
                                   const size_t *nc, const size_t *c_base, void *stream);
+/* The same for nblk resident element blocks (d_cblocks[b]: packed blocks of
+ * capacity block_cap): a search on the split-fp16 filter (real-valued data,
+ * knn_ctx_split) folds up to 8 of them in one distance launch and one merge,
+ * which count as ONE step of the lag rule; other searches fold one block a
+ * step (KNN_NO_FUSE=1 too). */
+KNN_API int knn_ctx_step_n(knn_ctx_t *ctx, int nblk, const void *const *d_cblocks, const size_t *nc,
+                           const size_t *c_base, void *stream);
 
 /* Finish: write nq*k records to d_out.  Returns in *unresolved (host; the
  * call synchronises the stream) the number of queries whose candidate set

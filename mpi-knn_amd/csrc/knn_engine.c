@@ -48,6 +48,8 @@ struct knn_ctx {
     float sscale;       /* its power-of-two pre-scale S */
     void *qsp, *csp[KNN_PSETS];   /* split shadow rows: the queries, converted corpus blocks */
     size_t qsp_bytes, csp_bytes;
+    void *cspm[KNN_PSETS];        /* a fused GEMM step's blocks in split form, side by side */
+    size_t cspm_bytes[KNN_PSETS];
     int lpq, klx;       /* partial lists of the active kernel: lpq per query and split, klx long */
     int i8_wgpc;        /* int8 distance workgroups a CU (2: the half-tile kernel) */
     int cus;
@@ -301,6 +303,7 @@ static void ctx_free_buffers(knn_ctx_t *c)
     for (int b = 0; b < KNN_PSETS; b++) hipFree(c->cs8[b]);
     hipFree(c->qsp);
     for (int b = 0; b < KNN_PSETS; b++) hipFree(c->csp[b]);
+    for (int b = 0; b < KNN_PSETS; b++) hipFree(c->cspm[b]);
     if (c->ev_in) hipEventDestroy(c->ev_in);
     if (c->ev_end) hipEventDestroy(c->ev_end);
     hipFree(c->qthr);
@@ -1318,6 +1321,107 @@ int knn_ctx_step_shadow_n(knn_ctx_t *c, int nblk, const void *const *d_sblocks, 
             xb.base[b] = (int64_t)c_base[b0 + b];
         }
         RCHK(ctx_step_impl(c, NULL, NULL, 0, 0, &xb, stream));
+    }
+    return KNN_OK;
+}
+
+/* Several resident element blocks in one step of a split-filter (GEMM
+ * mode) search: each block's split rows side by side, ONE k_dist_split
+ * launch over all of them (block table) and ONE k_merge re-ranking from all
+ * of them -- the direct exchange's received blocks at P = 8 were 7 launches
+ * of ~8 tiles a workgroup and 7 merges. */
+static int ctx_step_split_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks, const size_t *nc,
+                            const size_t *c_base, void *stream)
+{
+    HIPCHK(hipSetDevice(c->device));
+    RCHK(flush_pend2(c, NULL, NULL));
+    RCHK(merge_pending(c));
+    size_t nct = 0;   /* tile-rounded rows of the launch: the split model's input */
+    for (int b = 0; b < nblk; b++) nct += knn_round_up(nc[b], KNN_SPLIT_TC);
+    nct -= knn_round_up(nc[nblk - 1], KNN_SPLIT_TC) - nc[nblk - 1];
+    c->split_solo = 0;
+    const int nsplit = choose_splits(c, nct);
+    const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
+    c->nsplit_last = nsplit;
+    if (!(set & 1)) c->even_nsplit = nsplit;
+    RCHK(ensure_part_buffers(c, nsplit, set, c->even_nsplit));
+    hipStream_t cs = (hipStream_t)stream, ds = c->ds[ds_i];
+    HIPCHK(hipEventRecord(c->ev_in, cs));
+    HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
+    if (c->nstep >= KNN_PSETS) HIPCHK(hipStreamWaitEvent(ds, c->ev_m[set], 0));
+    const size_t per = knn_rows_pad(c->block_cap) * knn_split_rs(c->n);
+    if (c->cspm_bytes[set] < per * (size_t)nblk) {
+        /* (the set's last reader, merge s - 4, is ordered before ds above;
+         * a free waits for the device) */
+        HIPCHK(hipStreamSynchronize(ds));
+        hipFree(c->cspm[set]);
+        c->cspm[set] = NULL;
+        c->cspm_bytes[set] = 0;
+        if (hipMalloc(&c->cspm[set], per * (size_t)nblk) != hipSuccess) return KNN_ERR_NOMEM;
+        c->cspm_bytes[set] = per * (size_t)nblk;
+    }
+    const size_t norm_off = knn_rows_pad(c->block_cap) * knn_n_pad_dt(c->n, c->dtype) * knn_esize(c->dtype);
+    knn_split_blocks_t tab;
+    knn_merge_blocks_t mb;
+    memset(&tab, 0, sizeof(tab));
+    memset(&mb, 0, sizeof(mb));
+    tab.nblk = mb.nblk = nblk;
+    for (int b = 0; b < nblk; b++) {
+        char *sp = (char *)c->cspm[set] + per * (size_t)b;
+        RCHK(knn_launch_shadow_split(sp, d_cblocks[b], c->dtype, knn_rows_pad(nc[b]), c->n, c->sscale, ds));
+        tab.sp[b] = sp;
+        tab.nrm[b] = (const char *)d_cblocks[b] + norm_off;
+        tab.base[b] = mb.base[b] = (int64_t)c_base[b];
+        tab.nc[b] = mb.nc[b] = (int)nc[b];
+        tab.lim[b] = (int)knn_rows_pad(c->block_cap);
+        mb.ptr[b] = d_cblocks[b];
+    }
+    hipEvent_t *ev = NULL;
+    if (c->prof_on && c->prof_pending < KNN_PROF_STEPS) {
+        ev = &c->prof_ev[3 * c->prof_pending++];
+        HIPCHK(hipEventRecord(ev[0], ds));
+    }
+    RCHK(knn_launch_dist_split_n(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, c->qsp, &tab,
+                                 (int)c->n, c->meta, nsplit, c->part_d[set], c->part_i[set], c->part_T[set],
+                                 (int)c->nq_pad, c->qthr, c->xord, (float)(-2.0 / ((double)c->sscale * c->sscale)),
+                                 ds));
+    if (ev) HIPCHK(hipEventRecord(ev[1], ds));
+    HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
+    HIPCHK(hipEventRecord(c->ev_ds[set], ds));
+    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));
+    const int *perm = NULL;
+    if (want_order(c, nct)) {
+        if (!c->ord_ready) RCHK(find_order(c, set, nsplit));
+        perm = c->ord_perm;
+    }
+    RCHK(knn_launch_merge_n(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set], nsplit, c->lpq,
+                            c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x, c->st_i, c->st_T,
+                            c->qblk, c->q_rows_pad, &mb, (int)c->n, c->meta, c->qthr, c->split, perm, c->ms));
+    c->merged = 1;
+    HIPCHK(hipEventRecord(c->ev_m[set], c->ms));
+    if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
+    /* step s - 2 is merged by now (its merge read its blocks' rows) */
+    if (c->nstep >= KNN_STEP_LAG) HIPCHK(hipStreamWaitEvent(cs, c->ev_m[(c->nstep - KNN_STEP_LAG) % KNN_PSETS], 0));
+    c->first_step = 0;
+    c->nstep++;
+    return KNN_OK;
+}
+
+int knn_ctx_step_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks, const size_t *nc, const size_t *c_base,
+                   void *stream)
+{
+    if (!c || nblk < 1 || !d_cblocks || !nc || !c_base) return KNN_ERR_INVALID;
+    for (int b = 0; b < nblk; b++)
+        if (!d_cblocks[b] || nc[b] == 0 || nc[b] > c->block_cap) return KNN_ERR_INVALID;
+    /* the split filter (real-valued data, GEMM mode): fused launches of up to
+     * KNN_SPLIT_MAXBLK blocks; any other contraction folds one block a step */
+    if (!c->split || env_on("KNN_NO_FUSE") || env_on("KNN_SPLIT_V1")) {
+        for (int b = 0; b < nblk; b++) RCHK(ctx_step_impl(c, d_cblocks[b], NULL, nc[b], c_base[b], NULL, stream));
+        return KNN_OK;
+    }
+    for (int b0 = 0; b0 < nblk; b0 += KNN_SPLIT_MAXBLK) {
+        const int nb = nblk - b0 < KNN_SPLIT_MAXBLK ? nblk - b0 : KNN_SPLIT_MAXBLK;
+        RCHK(ctx_step_split_n(c, nb, d_cblocks + b0, nc + b0, c_base + b0, stream));
     }
     return KNN_OK;
 }

@@ -146,12 +146,44 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
                               qsh / csh (knn_launch_shadow_split); m2s = -2 / S^2   */
 #define KNN_DIST_SPLIT_V1 16 /* with SPLIT: k_dist_topk's 128-row-tile form instead of
                                 k_dist_split (KNN_SPLIT_V1=1; A/B runs)            */
-/* k_dist_split (knn_split.hip): the split fp16 filter on 256-row tiles */
+/* k_dist_split (knn_split.hip): the split fp16 filter on 256-row tiles,
+ * over up to KNN_SPLIT_MAXBLK corpus blocks in one launch (block b: split
+ * rows sp[b], norms nrm[b] of its element block, global ids base[b].., nc[b]
+ * rows, lim[b] rows allocated; tiles [t0[b], t0[b+1]) of the launch -- the
+ * launcher fills t0) */
 #define KNN_SPLIT_TC 256
+#define KNN_SPLIT_MAXBLK 8
+typedef struct {
+    const void *sp[KNN_SPLIT_MAXBLK];
+    const void *nrm[KNN_SPLIT_MAXBLK];
+    int64_t base[KNN_SPLIT_MAXBLK];
+    int nc[KNN_SPLIT_MAXBLK];
+    int lim[KNN_SPLIT_MAXBLK];
+    int t0[KNN_SPLIT_MAXBLK + 1];
+    int nblk;
+} knn_split_blocks_t;
+/* the element blocks a GEMM-mode merge re-ranks from (k_merge's exact S):
+ * block j holds global ids base[j] .. base[j] + nc[j] - 1 */
+typedef struct {
+    const void *ptr[KNN_SPLIT_MAXBLK];
+    int64_t base[KNN_SPLIT_MAXBLK];
+    int nc[KNN_SPLIT_MAXBLK];
+    int nblk;
+} knn_merge_blocks_t;
+int knn_launch_merge_n(int dtype, int kp, int k, const double *part_d, const int *part_i, const double *part_T,
+                       int nsplit, int lpq, int kl, int nq, int nq_pad, int first_step, double *st_d, double *st_x,
+                       int *st_i, double *st_T, const void *qblk, size_t q_rows_pad, const knn_merge_blocks_t *mb,
+                       int n, const double *meta, double *qthr, int filt, const int *qperm, void *stream);
+/* the split filter over several element blocks (their split rows in sp[],
+ * their norms in nrm[]): knn_launch_dist_topk's KNN_DIST_SPLIT for a table */
+int knn_launch_dist_split_n(int dtype, int kp, int k, const void *qblk, size_t q_rows_pad, size_t q_base, int nq,
+                            const void *qsp, const knn_split_blocks_t *cb, int n, const double *meta, int nsplit,
+                            double *part_d, int *part_i, double *part_T, int nq_pad, double *qthr, int xord,
+                            float m2s, void *stream);
 int knn_launch_dist_split(int dtype, int kl, const void *qsp, const void *qnorm, size_t q_base, int nq,
-                          const void *csp, const void *cnorm, size_t c_base, int nc, size_t c_rows_pad, int n,
-                          const double *meta, int nsplit, double *part_d, int *part_i, double *part_T,
-                          int nq_pad, double *qthr, int uj, int xord, float m2s, void *stream);
+                          const knn_split_blocks_t *cb, int n, const double *meta, int nsplit, double *part_d,
+                          int *part_i, double *part_T, int nq_pad, double *qthr, int uj, int xord, float m2s,
+                          void *stream);
 /* fp16 shadow rows (round_up(n, 64) halves a row) of a packed block */
 int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, void *stream);
 int knn_launch_fill_inf(double *p, int count, void *stream);

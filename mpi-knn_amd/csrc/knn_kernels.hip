@@ -1082,7 +1082,7 @@ __global__ __launch_bounds__(256) void k_merge(
     const double *__restrict__ part_T, int nsplit, int lpq, int kl, int nq, int nq_pad, int first_step,
     double *__restrict__ st_d, double *__restrict__ st_x, int *__restrict__ st_i,
     double *__restrict__ st_T, const TE *__restrict__ qblk, size_t qnorm_off,
-    const TE *__restrict__ cblk, size_t c_base, int nc, int n, int n_pad,
+    const knn_merge_blocks_t mb, int n, int n_pad,
     const double *__restrict__ meta, int k, unsigned long long *__restrict__ qthr, int filt,
     const int *__restrict__ qperm)
 {
@@ -1357,8 +1357,16 @@ __global__ __launch_bounds__(256) void k_merge(
             if (ssrc[x]) {
                 sx[x] = st_x[(size_t)q * KP + spos[x]];
             } else if (exact_ok && sd[x] <= win) {
-                const int row = (int)((long)si[x] - (long)c_base);
-                sx[x] = knn_exact_sq_v<TE>(qblk + (size_t)q * n_pad, cblk + (size_t)row * n_pad, n_pad);
+                // the row's block (new entries come from this step's blocks)
+                const TE *crow = (const TE *)mb.ptr[0];
+                long row = 0;
+#pragma unroll
+                for (int j = 0; j < KNN_SPLIT_MAXBLK; j++)
+                    if (j < mb.nblk && (long)si[x] >= mb.base[j] && (long)si[x] < mb.base[j] + mb.nc[j]) {
+                        crow = (const TE *)mb.ptr[j];
+                        row = (long)si[x] - mb.base[j];
+                    }
+                sx[x] = knn_exact_sq_v<TE>(qblk + (size_t)q * n_pad, crow + (size_t)row * n_pad, n_pad);
             } else {
                 sx[x] = KNN_INF;
             }
@@ -1379,7 +1387,6 @@ __global__ __launch_bounds__(256) void k_merge(
         }
         if (sl == 0) { st_T[2 * (size_t)q] = T; st_T[2 * (size_t)q + 1] = Td; }
     }
-    (void)nc;
 }
 
 // ---------------------------------------------------------------------------
@@ -2323,9 +2330,17 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
         // split fp16 shadow rows (4 bytes a feature); m2s = -2 / S^2 undoes
         // the scaling in the epilogue's fma (a power of two: exact)
         if (!qsh || !csh) return KNN_ERR_INVALID;
-        if (!(flags & KNN_DIST_SPLIT_V1))
-            return knn_launch_dist_split(dt, KL, qsh, qnorm, q_base, nq, csh, cnorm, c_base, nc, c_rows_pad, n,
-                                         meta, nsplit, part_d, part_i, part_T, nq_pad, qthr, uj, xord, m2s, s);
+        if (!(flags & KNN_DIST_SPLIT_V1)) {
+            knn_split_blocks_t cb{};
+            cb.nblk = 1;
+            cb.sp[0] = csh;
+            cb.nrm[0] = cnorm;
+            cb.base[0] = (int64_t)c_base;
+            cb.nc[0] = nc;
+            cb.lim[0] = (int)c_rows_pad;
+            return knn_launch_dist_split(dt, KL, qsh, qnorm, q_base, nq, &cb, n, meta, nsplit, part_d, part_i, part_T,
+                                         nq_pad, qthr, uj, xord, m2s, s);
+        }
         const int nps = (int)knn_round_up((size_t)n, 32);
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 3>), grid, dim3(512), 0, s,
                            (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
@@ -2395,6 +2410,39 @@ extern "C" int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, 
 #undef CALL
 }
 
+// the split filter over a table of element blocks (the engine's fused GEMM
+// step): the same lane-list slot of the shared bound and query norms as
+// launch_dist_topk's KNN_DIST_SPLIT branch
+template <typename T, int KL, int KP>
+static int launch_split_n(const T *qblk, size_t q_rows_pad, size_t q_base, int nq, const void *qsp,
+                          const knn_split_blocks_t *cb, int n, const double *meta, int nsplit, double *part_d,
+                          int *part_i, double *part_T, int nq_pad, double *qthr, int k, int xord, float m2s,
+                          hipStream_t s)
+{
+    constexpr int dt = sizeof(T) == 8 ? KNN_F64 : KNN_F32;
+    const int np = (int)knn_n_pad_dt(n, dt);
+    const int nqb = (nq + KNN_TQ - 1) / KNN_TQ;
+    if (nqb <= 0 || k <= 0 || k > KP || (size_t)nqb * KNN_TQ > q_rows_pad || nq_pad < nqb * KNN_TQ || !qsp)
+        return KNN_ERR_INVALID;
+    int uj_int = (k + 1 + 3) / 4 - 1;
+    if (uj_int > KL - 1) uj_int = KL - 1;
+    const int uj = uj_int | ((KL - 1) << 8);
+    return knn_launch_dist_split(dt, KL, qsp, qblk + q_rows_pad * np, q_base, nq, cb, n, meta, nsplit, part_d, part_i,
+                                 part_T, nq_pad, qthr, uj, xord, m2s, s);
+}
+
+extern "C" int knn_launch_dist_split_n(int dtype, int kp, int k, const void *qblk, size_t q_rows_pad, size_t q_base,
+                                       int nq, const void *qsp, const knn_split_blocks_t *cb, int n,
+                                       const double *meta, int nsplit, double *part_d, int *part_i, double *part_T,
+                                       int nq_pad, double *qthr, int xord, float m2s, void *stream)
+{
+#define CALL(T, KL, KP)                                                                                    \
+    return launch_split_n<T, KL, KP>((const T *)qblk, q_rows_pad, q_base, nq, qsp, cb, n, meta, nsplit, part_d, \
+                                     part_i, part_T, nq_pad, qthr, k, xord, m2s, (hipStream_t)stream)
+    KNN_DISPATCH(dtype, kp, CALL);
+#undef CALL
+}
+
 extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, const int *part_i,
                                 const double *part_T, int nsplit, int lpq, int kl, int nq, int nq_pad,
                                 int first_step, double *st_d, double *st_x, int *st_i,
@@ -2402,6 +2450,23 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
                                 const void *cblk, size_t c_base, int nc, int n,
                                 const double *meta, double *qthr, int filt, const int *qperm, void *stream)
 {
+    knn_merge_blocks_t mb{};
+    mb.nblk = 1;
+    mb.ptr[0] = cblk;
+    mb.base[0] = (int64_t)c_base;
+    mb.nc[0] = nc;
+    return knn_launch_merge_n(dtype, kp, k, part_d, part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d,
+                              st_x, st_i, st_T, qblk, q_rows_pad, &mb, n, meta, qthr, filt, qperm, stream);
+}
+
+extern "C" int knn_launch_merge_n(int dtype, int kp, int k, const double *part_d, const int *part_i,
+                                  const double *part_T, int nsplit, int lpq, int kl, int nq, int nq_pad,
+                                  int first_step, double *st_d, double *st_x, int *st_i, double *st_T,
+                                  const void *qblk, size_t q_rows_pad, const knn_merge_blocks_t *mbp, int n,
+                                  const double *meta, double *qthr, int filt, const int *qperm, void *stream)
+{
+    if (!mbp || mbp->nblk < 1 || mbp->nblk > KNN_SPLIT_MAXBLK) return KNN_ERR_INVALID;
+    const knn_merge_blocks_t mb = *mbp;
     if (lpq < 1 || kl < 1 || lpq * nsplit + 1 > 64 || k <= 0 || k > kp) return KNN_ERR_INVALID;
     const int np = (int)knn_n_pad_dt(n, dtype);
     const size_t qn_off = q_rows_pad * (size_t)np;
@@ -2415,22 +2480,22 @@ extern "C" int knn_launch_merge(int dtype, int kp, int k, const double *part_d, 
     if (pf && KP == 32 && two)                                                                   \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, 32, 32, 8>), grid, dim3(256), 0, s, part_d,  \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
-                           st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
+                           st_i, st_T, (const T *)qblk, qn_off, mb, n,                             \
                            np, meta, k, (unsigned long long *)qthr, filt, qperm);                         \
     else if (pf && KP == 32)                                                                     \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, 32, 64, 8>), grid, dim3(256), 0, s, part_d,  \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
-                           st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
+                           st_i, st_T, (const T *)qblk, qn_off, mb, n,                             \
                            np, meta, k, (unsigned long long *)qthr, filt, qperm);                         \
     else if (two)                                                                                \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP, 32>), grid, dim3(256), 0, s, part_d,     \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
-                           st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
+                           st_i, st_T, (const T *)qblk, qn_off, mb, n,                             \
                            np, meta, k, (unsigned long long *)qthr, filt, qperm);                         \
     else                                                                                         \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge<T, KP, 64>), grid, dim3(256), 0, s, part_d,     \
                            part_i, part_T, nsplit, lpq, kl, nq, nq_pad, first_step, st_d, st_x,    \
-                           st_i, st_T, (const T *)qblk, qn_off, (const T *)cblk, c_base, nc, n,    \
+                           st_i, st_T, (const T *)qblk, qn_off, mb, n,                             \
                            np, meta, k, (unsigned long long *)qthr, filt, qperm);                         \
     return hip_status()
     KNN_DISPATCH(dtype, kp, CALL);

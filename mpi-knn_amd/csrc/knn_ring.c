@@ -382,6 +382,8 @@ static int direct_pass(ring_dev_t *d, int P, size_t R, size_t m, size_t n, int d
             rc = knn_ctx_step_shadow_n(e->ctx, P, blk, nc, base, e->cs);
         } else if (form && !rescan) {
             rc = knn_ctx_step_shadow_n(e->ctx, P - 1, blk + 1, nc + 1, base + 1, e->cs);
+        } else if (!rescan) {
+            rc = knn_ctx_step_n(e->ctx, P - 1, blk + 1, nc + 1, base + 1, e->cs);
         } else {
             rc = KNN_OK;
             for (int j = 1; j < P && !rc; j++) rc = fold_one(e, blk[j], nc[j], base[j], rescan, form);

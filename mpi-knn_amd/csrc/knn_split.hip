@@ -84,8 +84,7 @@ typedef int knn_si4 __attribute__((ext_vector_type(4)));
 template <typename T, int KL, int D>
 __global__ __launch_bounds__(512) void k_dist_split(
     const char *__restrict__ qsp, const T *__restrict__ qnorm, size_t q_base, int nq,
-    const char *__restrict__ csp, const T *__restrict__ cnorm, size_t c_base, int nc, int c_rows_lim,
-    int n, int rsb, int ntiles, int nsplit, int nqb, const double *__restrict__ meta,
+    const knn_split_blocks_t cb, int n, int rsb, int nsplit, int nqb, const double *__restrict__ meta,
     double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T, int nq_pad,
     unsigned long long *__restrict__ qthr, int uj, int xord, float m2s)
 {
@@ -107,6 +106,15 @@ __global__ __launch_bounds__(512) void k_dist_split(
         qb = blockIdx.x % nqb;
         split = blockIdx.x / nqb;
     }
+    const int ntiles = cb.t0[cb.nblk];
+    // block of launch tile t (wave-uniform: the table is in the kernel
+    // arguments, <= KNN_SPLIT_MAXBLK entries)
+    auto blk_of = [&](int t) {
+        int b = 0;
+#pragma unroll
+        for (int j = 1; j < KNN_SPLIT_MAXBLK; j++) b = (j < cb.nblk && t >= cb.t0[j]) ? j : b;
+        return b;
+    };
     const int tb = ntiles / nsplit, tr = ntiles - tb * nsplit;
     const int t_lo = split * tb + (split < tr ? split : tr);
     const int t_hi = t_lo + tb + (split < tr ? 1 : 0);
@@ -141,17 +149,23 @@ __global__ __launch_bounds__(512) void k_dist_split(
     const int lr = lane >> 3, ls = lane & 7;
     const int seg_b = 16 * (ls ^ lr);
     int s_c = 0, s_t = t_lo, s_fc = 0, s_st = 0;      // chunk being staged, its stage
+    // the staged tile's block, row 0 and last allocated row (scalar; the
+    // table is read only when the cursor crosses into the next block -- a
+    // table load per piece put an lgkmcnt(0) behind every fragment read)
+    int s_b = blk_of(t_lo);
+    const char *s_row = (const char *)cb.sp[s_b] + (size_t)(t_lo - cb.t0[s_b]) * SP_TC * rsb;
+    int s_lim = cb.lim[s_b] - 1 - (t_lo - cb.t0[s_b]) * SP_TC;
+    int s_next = s_b + 1 < cb.nblk ? cb.t0[s_b + 1] : 0x7fffffff;
     // piece i (0..3) of a chunk: corpus rows 32 w + 8 i.. of the tile; rows
     // past the block's allocation are clamped to its last row (their
     // candidates are masked by index)
     auto glds1 = [&](int i) {
         if (SP_ABL_NODMA) return;
         const unsigned dst0 = (unsigned)(uintptr_t)lds + (unsigned)s_st * SP_STAGE;
-        const char *cb = csp + (size_t)s_t * SP_TC * rsb + (size_t)128 * s_fc;
-        const int lim = c_rows_lim - 1 - s_t * SP_TC;
+        const char *cp = s_row + (size_t)128 * s_fc;
         int lrow = 32 * wave_s + 8 * i + lr;
-        lrow = lrow < lim ? lrow : lim;
-        bglds16(knn_rsrc(cb), (unsigned)(lrow * rsb + seg_b),
+        lrow = lrow < s_lim ? lrow : s_lim;
+        bglds16(knn_rsrc(cp), (unsigned)(lrow * rsb + seg_b),
                 dst0 + (unsigned)(2 * wave_s + (i >> 1)) * 2048u + (unsigned)(i & 1) * 1024u);
     };
     auto advance = [&]() {
@@ -160,7 +174,15 @@ __global__ __launch_bounds__(512) void k_dist_split(
         if (s_c < total) {
             if (++s_fc == nfc) {
                 s_fc = 0;
-                s_t++;
+                if (++s_t == s_next) {   // the next block of the launch
+                    s_b++;
+                    s_row = (const char *)cb.sp[s_b];
+                    s_lim = cb.lim[s_b] - 1;
+                    s_next = s_b + 1 < cb.nblk ? cb.t0[s_b + 1] : 0x7fffffff;
+                } else {
+                    s_row += (size_t)SP_TC * rsb;
+                    s_lim -= SP_TC;
+                }
             }
         }
     };
@@ -183,12 +205,13 @@ __global__ __launch_bounds__(512) void k_dist_split(
     auto gnorm = [&](int t) {
         if (wave_s >= NU / 64) return;
         const int ts = t < t_hi ? t : t_hi - 1;
+        const int b = blk_of(ts);
         const int u = 64 * wave_s + lane;
         const int p = ES == 8 ? u >> 1 : u;
         const int gg = p >> 6, k = p & 63;
-        int row = ts * SP_TC + 16 * (k >> 2) + 4 * gg + (k & 3);
-        row = row < c_rows_lim ? row : c_rows_lim - 1;
-        const char *src = (const char *)(cnorm + row) + (ES == 8 ? (u & 1) * 4 : 0);
+        int row = (ts - cb.t0[b]) * SP_TC + 16 * (k >> 2) + 4 * gg + (k & 3);
+        row = row < cb.lim[b] ? row : cb.lim[b] - 1;
+        const char *src = (const char *)((const T *)cb.nrm[b] + row) + (ES == 8 ? (u & 1) * 4 : 0);
         glds4(src, (unsigned)(uintptr_t)lds + SP_NORM_OFF + (unsigned)(t & 3) * SP_NORM_SLOT +
                        (unsigned)wave_s * 256u);
     };
@@ -204,7 +227,10 @@ __global__ __launch_bounds__(512) void k_dist_split(
         }
         const LDS_AS T *cng = (const LDS_AS T *)(lds + SP_NORM_OFF + (t & 3) * SP_NORM_SLOT) + 64 * g;
         const float lim = L[KL - 1] < thr ? L[KL - 1] : thr;
-        const int row0 = t * SP_TC;
+        const int eb = blk_of(t);
+        const long c_base = cb.base[eb];
+        const int nc = cb.nc[eb];
+        const int row0 = (t - cb.t0[eb]) * SP_TC;
         const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 16 * wave_s;
         const bool masked = (row0 + SP_TC > nc) || (gw0 < gt0 + SP_TC && gt0 < gw0 + 16);
 #pragma unroll
@@ -302,7 +328,8 @@ __global__ __launch_bounds__(512) void k_dist_split(
             advance();
         }
         // B(0), norms, chunk 0 landed: chunks 1, 2 (8 pieces) may stay in flight
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (SP_ABL_NODMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         asm volatile("" : "+v"(qh_c), "+v"(ql_c));
         __builtin_amdgcn_s_barrier();
 
@@ -360,7 +387,8 @@ __global__ __launch_bounds__(512) void k_dist_split(
                 __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this stage's reads done
                 // the next chunk's query fragments and pieces landed (and
                 // chunk c + 2's): chunk c + 3's 4 pieces may stay in flight
-                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                if (SP_ABL_NODMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (no pieces to count)
+                else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                 asm volatile("" : "+v"(qh_n), "+v"(ql_n));
                 qh_c = qh_n;
                 ql_c = ql_n;
@@ -393,38 +421,42 @@ __global__ __launch_bounds__(512) void k_dist_split(
 }
 
 template <typename T, int KL, int D>
-static int launch_split(const void *qsp, const T *qnorm, size_t q_base, int nq, const void *csp,
-                        const T *cnorm, size_t c_base, int nc, size_t c_rows_pad, int n, const double *meta,
-                        int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad, double *qthr, int uj,
-                        int xord, float m2s, hipStream_t s)
+static int launch_split(const void *qsp, const T *qnorm, size_t q_base, int nq, const knn_split_blocks_t &cb, int n,
+                        const double *meta, int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
+                        double *qthr, int uj, int xord, float m2s, hipStream_t s)
 {
     const int rsb = (int)knn_split_rs((size_t)n);
     const int nqb = (nq + SP_TQ - 1) / SP_TQ;
-    const int ntiles = (nc + SP_TC - 1) / SP_TC;
     const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_split<T, KL, D>), dim3((unsigned)(nqb_grid * nsplit)), dim3(512), 0, s,
-                       (const char *)qsp, qnorm, q_base, nq, (const char *)csp, cnorm, c_base, nc,
-                       (int)c_rows_pad, n, rsb, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                       (unsigned long long *)qthr, uj, xord, m2s);
+                       (const char *)qsp, qnorm, q_base, nq, cb, n, rsb, nsplit, nqb, meta, part_d, part_i, part_T,
+                       nq_pad, (unsigned long long *)qthr, uj, xord, m2s);
     return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
 }
 
-// The launcher behind knn_launch_dist_topk's KNN_DIST_SPLIT (knn_kernels.hip
-// checks the query-block geometry); corpus rows are staged in 256-row tiles
-// (knn_split_tiles), the last tile's rows past c_rows_pad clamped in the
-// kernel.
+// The launcher behind knn_launch_dist_topk's KNN_DIST_SPLIT (one block) and
+// the engine's fused GEMM step (several): the table's tiles are 256-row
+// tiles of each block in turn (t0 filled here), the last tile of a block
+// clamped to its allocation in the kernel.
 extern "C" int knn_launch_dist_split(int dtype, int kl, const void *qsp, const void *qnorm, size_t q_base,
-                                     int nq, const void *csp, const void *cnorm, size_t c_base, int nc,
-                                     size_t c_rows_pad, int n, const double *meta, int nsplit, double *part_d,
-                                     int *part_i, double *part_T, int nq_pad, double *qthr, int uj, int xord,
-                                     float m2s, void *stream)
+                                     int nq, const knn_split_blocks_t *cbp, int n, const double *meta, int nsplit,
+                                     double *part_d, int *part_i, double *part_T, int nq_pad, double *qthr, int uj,
+                                     int xord, float m2s, void *stream)
 {
-    if (nq <= 0 || nc <= 0 || nsplit <= 0 || (size_t)nc > c_rows_pad || !qsp || !csp) return KNN_ERR_INVALID;
-    if ((nc + SP_TC - 1) / SP_TC < nsplit) return KNN_ERR_INVALID;
+    if (nq <= 0 || nsplit <= 0 || !qsp || !cbp || cbp->nblk < 1 || cbp->nblk > KNN_SPLIT_MAXBLK)
+        return KNN_ERR_INVALID;
+    knn_split_blocks_t cb = *cbp;
+    cb.t0[0] = 0;
+    for (int b = 0; b < cb.nblk; b++) {
+        if (!cb.sp[b] || !cb.nrm[b] || cb.nc[b] <= 0 || cb.nc[b] > cb.lim[b] || cb.base[b] < 0) return KNN_ERR_INVALID;
+        cb.t0[b + 1] = cb.t0[b] + (cb.nc[b] + SP_TC - 1) / SP_TC;
+    }
+    for (int b = cb.nblk + 1; b <= KNN_SPLIT_MAXBLK; b++) cb.t0[b] = cb.t0[cb.nblk];
+    if (cb.t0[cb.nblk] < nsplit) return KNN_ERR_INVALID;
     hipStream_t s = (hipStream_t)stream;
-#define SPL(T, KL)                                                                                         \
-    return launch_split<T, KL, (KL > 24 ? 2 : 4)>(qsp, (const T *)qnorm, q_base, nq, csp, (const T *)cnorm, c_base, nc, c_rows_pad, \
-                               n, meta, nsplit, part_d, part_i, part_T, nq_pad, qthr, uj, xord, m2s, s)
+#define SPL(T, KL)                                                                                          \
+    return launch_split<T, KL, (KL > 24 ? 2 : 4)>(qsp, (const T *)qnorm, q_base, nq, cb, n, meta, nsplit, part_d, \
+                                                 part_i, part_T, nq_pad, qthr, uj, xord, m2s, s)
     if (dtype == KNN_F64 && kl == KNN_KL) SPL(double, KNN_KL);
     if (dtype == KNN_F32 && kl == KNN_KL) SPL(float, KNN_KL);
     if (dtype == KNN_F32 && kl == KNN_KL_M) SPL(float, KNN_KL_M);

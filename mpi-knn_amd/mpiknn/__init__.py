@@ -48,7 +48,7 @@ API_SYMBOLS = (
     "knn_ctx_shadow", "knn_ctx_step_shadow", "knn_ctx_begin_meta", "knn_ctx_shadow_bytes",
     "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n", "knn_ctx_split", "knn_s8_block_bytes",
     "knn_s8_block_meta_offset", "knn_block_pack_s8", "knn_s8_spec_ok", "knn_ctx_begin_s8",
-    "knn_ctx_attach_qblock", "knn_ctx_research_blocks",
+    "knn_ctx_attach_qblock", "knn_ctx_research_blocks", "knn_ctx_step_n",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -129,6 +129,7 @@ def _load():
         "knn_ctx_begin_s8": ([p, p, sz, sz, p, p, p], i),
         "knn_ctx_attach_qblock": ([p, p, sz], i),
         "knn_ctx_research_blocks": ([p, i, pp, psz, psz, p, psz, p], i),
+        "knn_ctx_step_n": ([p, i, pp, psz, psz, p], i),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -374,6 +375,15 @@ class Context:
         cbv = (ctypes.c_size_t * nb)(*c_bases)
         _check(lib.knn_ctx_step_shadow_n(self._h, nb, ptrs, ncv, cbv, stream or None),
                "knn_ctx_step_shadow_n")
+
+    def step_n(self, d_cblocks, ncs, c_bases, stream=0):
+        """several resident element blocks in one step (split-filter
+        searches: one fused distance launch and merge per 8 blocks)"""
+        nb = len(d_cblocks)
+        ptrs = (ctypes.c_void_p * nb)(*d_cblocks)
+        ncv = (ctypes.c_size_t * nb)(*ncs)
+        cbv = (ctypes.c_size_t * nb)(*c_bases)
+        _check(lib.knn_ctx_step_n(self._h, nb, ptrs, ncv, cbv, stream or None), "knn_ctx_step_n")
 
     def research_blocks(self, d_sblocks, ncs, c_bases, d_out, stream=0):
         """A ring rank's int8 re-search of the queries end() left

@@ -244,6 +244,9 @@ class GpuEngine:
     def step_shadow_n(self, sbufs, rows, bases):
         self.ctx.step_shadow_n([b.data_ptr() for b in sbufs], rows, bases, self.stream())
 
+    def step_n(self, bufs, rows, bases):
+        self.ctx.step_n([b.data_ptr() for b in bufs], rows, bases, self.stream())
+
     def step(self, buf, rows, base, rescan=False):
         if rescan:
             self.ctx.rescan_step(buf.data_ptr(), rows, base, self.stream())
@@ -450,6 +453,9 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
             engine.step_shadow_n([x for x, _, _ in nz], [r for _, _, r in nz], [b for _, b, _ in nz])
         elif use_shadow and len(nz) > 0:
             engine.step_shadow_n([x for x, _, _ in nz], [r for _, _, r in nz], [b for _, b, _ in nz])
+        elif not rescan and len(nz) > 1 and hasattr(engine, "step_n"):
+            # element blocks (real-valued data: one fused split-filter step)
+            engine.step_n([x for x, _, _ in nz], [r for _, _, r in nz], [b for _, b, _ in nz])
         else:
             for buf, b, r in nz:
                 engine.step(buf, r, b, rescan)

@@ -134,6 +134,8 @@ def main():
         eng.end()
 
         fuse = args.fuse if shadow and P > 1 and eng.ctx.shadow() == 2 else "none"
+        # element blocks of a split-filter search: the direct schedule's fused step
+        efuse = args.fuse if not shadow and P > 1 and eng.ctx.split() else "none"
 
         def one():
             eng.begin(0, h_meta=h_meta)
@@ -144,6 +146,11 @@ def main():
                 eng.step_shadow(sbufs[0], blocks[0][1], blocks[0][0])
                 eng.ctx.step_shadow_n([b.data_ptr() for b in sbufs[1:]], [r for _, r in blocks[1:]],
                                       [bs for bs, _ in blocks[1:]], eng.stream())
+            elif efuse == "rest":
+                eng.step(bufs[0], blocks[0][1], blocks[0][0])
+                eng.step_n(bufs[1:], [r for _, r in blocks[1:]], [bs for bs, _ in blocks[1:]])
+            elif efuse == "all":
+                eng.step_n(bufs, [r for _, r in blocks], [bs for bs, _ in blocks])
             else:
                 for b, (base, rows) in enumerate(blocks):
                     if shadow:
@@ -183,7 +190,7 @@ def main():
                   "dist_busy_ms_per_pass": dist_ms / args.steps,
                   "dist_tflops": flops / (dist_ms * 1e-3) / 1e12 if dist_ms > 0 else None,
                   "exposed_merge_ms_per_pass": merge_ms / args.steps,
-                  "splits": eng.ctx.info()[1], "shadow_ring": shadow, "fuse": fuse,
+                  "splits": eng.ctx.info()[1], "shadow_ring": shadow, "fuse": fuse if shadow else efuse,
                   "contraction_bits": eng.ctx.contraction_bits(), "unresolved": unres,
                   "unresolved_after_research": unres2}
         print(json.dumps({"P": P, **res[P]}), file=sys.stderr, flush=True)
