@@ -1146,6 +1146,13 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
      * work filters with the running answer instead of cold lane lists
      * (making the launch wait for that merge measured no faster, DESIGN.md
      * sec.5). */
+    /* a split-filter (GEMM) search's first step on its own query block keeps
+     * its merge pending: the direct exchange's fused step (knn_ctx_step_n)
+     * merges both in one k_merge over a table of all their blocks -- the
+     * own block's merge could not run beside the fused launch anyway (its
+     * workgroups hold every register of every CU), so it ran alone after
+     * it; any other next step merges it first, as a single merge */
+    const int gemm_own = c->split && !xb && c->nstep == 0 && d_cblock == c->qblk && !env_on("KNN_NO_PAIR_FUSED");
     int pairing = 0;
     if ((set & 1) && c->pend) {
         pairing = (can_pair && nsplit == c->pend_nsplit && !xb) || pair_fused;
@@ -1264,7 +1271,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
             if (c->pend_ev) HIPCHK(hipEventRecord(c->pend_ev[2], c->ms));
             if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
         }
-    } else if (!(set & 1) && can_pair) {
+    } else if (!(set & 1) && (can_pair || gemm_own)) {
         c->pend = 1;
         c->pend_set = set;
         c->pend_nsplit = nsplit;
@@ -1335,13 +1342,17 @@ static int ctx_step_split_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks
 {
     HIPCHK(hipSetDevice(c->device));
     RCHK(flush_pend2(c, NULL, NULL));
-    RCHK(merge_pending(c));
     size_t nct = 0;   /* tile-rounded rows of the launch: the split model's input */
     for (int b = 0; b < nblk; b++) nct += knn_round_up(nc[b], KNN_SPLIT_TC);
     nct -= knn_round_up(nc[nblk - 1], KNN_SPLIT_TC) - nc[nblk - 1];
     c->split_solo = 0;
     const int nsplit = choose_splits(c, nct);
     const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
+    /* the pending own-block step (odd set right behind its lists) shares
+     * this step's merge when the lists and the block table fit */
+    const int share = c->pend && (set & 1) && nblk + 1 <= KNN_SPLIT_MAXBLK &&
+                      c->lpq * (c->pend_nsplit + nsplit) + 1 <= 64;
+    if (!share) RCHK(merge_pending(c));
     c->nsplit_last = nsplit;
     if (!(set & 1)) c->even_nsplit = nsplit;
     RCHK(ensure_part_buffers(c, nsplit, set, c->even_nsplit));
@@ -1389,16 +1400,33 @@ static int ctx_step_split_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks
     HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
     HIPCHK(hipEventRecord(c->ev_ds[set], ds));
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));
+    int mset = set, mnsplit = nsplit;
+    hipEvent_t *pev = NULL;
+    if (share) {
+        /* one merge of both steps: the pending set's lists, then this one's */
+        HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i ^ 1], 0));
+        c->pend = 0;
+        mb.ptr[nblk] = c->pend_cblk;
+        mb.base[nblk] = (int64_t)c->pend_cbase;
+        mb.nc[nblk] = c->pend_nc;
+        mb.nblk = nblk + 1;
+        mset = c->pend_set;
+        mnsplit = c->pend_nsplit + nsplit;
+        nct += (size_t)c->pend_nc;
+        pev = c->pend_ev;
+    }
     const int *perm = NULL;
     if (want_order(c, nct)) {
-        if (!c->ord_ready) RCHK(find_order(c, set, nsplit));
+        if (!c->ord_ready) RCHK(find_order(c, mset, mnsplit));
         perm = c->ord_perm;
     }
-    RCHK(knn_launch_merge_n(c->dtype, c->kp, c->k, c->part_d[set], c->part_i[set], c->part_T[set], nsplit, c->lpq,
-                            c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x, c->st_i, c->st_T,
-                            c->qblk, c->q_rows_pad, &mb, (int)c->n, c->meta, c->qthr, c->split, perm, c->ms));
+    RCHK(knn_launch_merge_n(c->dtype, c->kp, c->k, c->part_d[mset], c->part_i[mset], c->part_T[mset], mnsplit,
+                            c->lpq, c->klx, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d, c->st_x, c->st_i,
+                            c->st_T, c->qblk, c->q_rows_pad, &mb, (int)c->n, c->meta, c->qthr, c->split, perm, c->ms));
     c->merged = 1;
     HIPCHK(hipEventRecord(c->ev_m[set], c->ms));
+    if (share) HIPCHK(hipEventRecord(c->ev_m[mset], c->ms));
+    if (pev) HIPCHK(hipEventRecord(pev[2], c->ms));
     if (ev) HIPCHK(hipEventRecord(ev[2], c->ms));
     /* step s - 2 is merged by now (its merge read its blocks' rows) */
     if (c->nstep >= KNN_STEP_LAG) HIPCHK(hipStreamWaitEvent(cs, c->ev_m[(c->nstep - KNN_STEP_LAG) % KNN_PSETS], 0));
