@@ -307,11 +307,24 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
     R, blocks = partition(m, P)
     wire = False
     h_meta = None
+    verify = None
+    ring_hint = None
     if P > 1:
         dist.all_reduce(engine.meta, op=dist.ReduceOp.MAX)
-        h_meta = engine.meta.cpu().numpy()   # the ring needs it on the host anyway
+        ring_hint = getattr(engine, "ring_hint", None)
+        if ring_hint is not None and hasattr(engine, "meta_host"):
+            # the reduced meta of this engine's last search as the hint (the
+            # same data, search after search): the contraction is chosen from
+            # it at once, the device-side reduction orders the kernels (under
+            # nccl the all-reduce is stream-ordered, no host wait), and its
+            # result is read back behind the search and checked after end()
+            # -- a mismatch (new data) runs the search again, on every rank
+            # alike: the reduced meta and the hint are the same everywhere
+            h_meta = ring_hint
+            verify = engine.meta_host(engine.meta)
+        else:
+            h_meta = engine.meta.cpu().numpy()   # the ring needs it on the host anyway
     spec = getattr(engine, "spec", False)
-    verify = None
     if h_meta is None and spec:
         hint = getattr(engine, "spec_hint", None)
         if hint is not None:
@@ -478,12 +491,18 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
         # any element-block exchange for the exact rescan
         unresolved = engine.research([x for x, _, _ in held_s], [r for _, _, r in held_s],
                                      [b for _, b, _ in held_s])
-    if verify is not None:
+    if verify is not None and P == 1:
         # (the read-back was enqueued before the search's first kernel, which
         # the merge end() synchronised with waits for: it has landed)
         if not engine.mk.s8_spec_ok(verify.numpy(), engine.n, engine.dtype):
             engine.spec_hint = None   # not this data: the checked path, from the start
             return ring_search(dist, torch, engine, rank, P, m, q_base, schedule, timeout_s)
+    if verify is not None and P > 1:
+        if not np.array_equal(np.asarray(verify.numpy() if hasattr(verify, "numpy") else verify), ring_hint):
+            engine.ring_hint = None   # new data: again, from the reduced meta itself
+            return ring_search(dist, torch, engine, rank, P, m, q_base, schedule, timeout_s)
+    if P > 1 and h_meta is not None and hasattr(engine, "meta_host"):
+        engine.ring_hint = np.array(h_meta, dtype=np.float64, copy=True)
     total = unresolved
     if P > 1:
         t = torch.tensor([float(unresolved)], dtype=torch.float64, device=engine.meta.device)

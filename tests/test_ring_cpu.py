@@ -30,6 +30,7 @@ class CpuEngine:
         self.meta = torch.zeros(8, dtype=torch.float64)
         self.force_rescan = force_rescan
         self.visits = {False: [], True: []}
+        self.h_metas = []
 
     def pack(self, src):
         rows = src.shape[0]
@@ -41,6 +42,11 @@ class CpuEngine:
     def begin(self, q_base, h_meta=None):
         self.q_base = q_base
         self.lists = self.O.lists_init(self.nq, self.k)
+        self.h_metas.append(None if h_meta is None else np.array(h_meta))
+
+    def meta_host(self, meta):
+        # (GpuEngine: an asynchronous copy into pinned memory)
+        return meta.clone()
 
     def step(self, buf, rows, base, rescan=False):
         assert int(buf[0, self.n]) == rows           # the block we were told we hold
@@ -116,6 +122,64 @@ def test_ring_schedule_gloo(world, force_rescan, schedule, monkeypatch):
         assert every, "rank %d did not fold every block once" % rank
         assert every_rescan, "rank %d rescan pass missed a block" % rank
         assert meta_ok, "rank %d meta not max-reduced" % rank
+
+
+def _hint_worker(rank, world, port, q):
+    """three searches on one engine: the first from the reduced meta, the
+    second from the first one's meta as the hint (verified after end()), the
+    third on rescaled rows -- the hint no longer matches, every rank runs the
+    search again from the reduced meta; every result the serial scan's"""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(here, "..", "oracle"), os.path.join(here, "..", "mpi-knn_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import datasets
+        import oracle
+        from mpiknn.ring import partition, ring_search
+        X, _ = datasets.digits_real()
+        m, n = X.shape
+        R, blocks = partition(m, world)
+        base, rows = blocks[rank]
+        eng = CpuEngine(oracle, n, R, rows, 30, False)
+        oks = []
+        for Xs in (X, X, 3.0 * X):
+            eng.visits = {False: [], True: []}
+            eng.pack(torch.from_numpy(Xs[base:base + rows]))
+            ring_search(dist, torch, eng, rank, world, m, base)
+            full = oracle.knn(Xs, 30, rows=(base, rows))
+            oks.append(np.array_equal(eng.lists[["distance", "idx"]], full[["distance", "idx"]]))
+        # begins: reduced meta, the hint, the (stale) hint, then the redo
+        hm = eng.h_metas
+        shape = (len(hm) == 4 and hm[1] is not None and np.array_equal(hm[1], hm[0]) and
+                 np.array_equal(hm[2], hm[0]) and not np.array_equal(hm[3], hm[0]))
+        q.put((rank, all(oks), shape))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("schedule", ["direct", "ring"])
+def test_ring_meta_hint_gloo(schedule, monkeypatch):
+    """P > 1 searches after the first start from the last reduced meta
+    (no host wait on the all-reduce); new data is caught after end() and
+    searched again on every rank."""
+    monkeypatch.setenv("KNN_RING_SCHEDULE", schedule)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_hint_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, shape in sorted(res):
+        assert ok, "rank %d lists differ from the serial scan" % rank
+        assert shape, "rank %d: begins did not follow reduced / hint / stale hint / redo" % rank
 
 
 def test_partition_covers_all_rows():
