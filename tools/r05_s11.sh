@@ -1,7 +1,7 @@
-# round-5 session 11: k_dist_split32 (32x32x16 MFMA, lists <= 24) parity + A/B against the 16x16 form
+# round-5 session 11: k_dist_split32 + shared own-block GEMM merge + ring meta hint -- parity, A/B, P=8 emulation
 set -o pipefail
 mkdir -p gpurun_out/s11
-timeout -k 10 700 python -u -m pytest tests/test_gpu_f32.py tests/test_golden.py tests/test_gpu_parity.py tests/test_gpu_fullsize_ring.py tests/test_gpu_ring_rotation.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/s11/tests.log 2>&1 || { tail -40 gpurun_out/s11/tests.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests/test_gpu_f32.py tests/test_golden.py tests/test_gpu_parity.py tests/test_gpu_fullsize_ring.py tests/test_gpu_ring_rotation.py tests/test_gpu_rccl_self.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/s11/tests.log 2>&1 || { tail -40 gpurun_out/s11/tests.log; exit 1; }
 tail -1 gpurun_out/s11/tests.log
 for r in 1 2; do
 for v in 0 1; do
@@ -11,5 +11,5 @@ for v in 0 1; do
 done
 done
 unset KNN_SPLIT16
-timeout -k 10 200 python -u tools/ring_emulate.py --workload mnist-real --ranks 1,8 --steps 5 > gpurun_out/s11/emu_mr.log 2>&1 || { tail -20 gpurun_out/s11/emu_mr.log; exit 1; }
+timeout -k 10 300 python -u tools/ring_emulate.py --workload mnist-real --ranks 1,2,4,8 --steps 5 > gpurun_out/s11/emu_mr.log 2>&1 || { tail -20 gpurun_out/s11/emu_mr.log; exit 1; }
 grep '"P"' gpurun_out/s11/emu_mr.log
