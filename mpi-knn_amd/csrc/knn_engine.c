@@ -1350,12 +1350,21 @@ static int ctx_step_split_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks
     const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
     /* the pending own-block step (odd set right behind its lists) shares
      * this step's merge when the lists and the block table fit */
-    const int share = c->pend && (set & 1) && nblk + 1 <= KNN_SPLIT_MAXBLK &&
-                      c->lpq * (c->pend_nsplit + nsplit) + 1 <= 64;
+    int share = c->pend && (set & 1) && nblk + 1 <= KNN_SPLIT_MAXBLK &&
+                c->lpq * (c->pend_nsplit + nsplit) + 1 <= 64;
     if (!share) RCHK(merge_pending(c));
     c->nsplit_last = nsplit;
     if (!(set & 1)) c->even_nsplit = nsplit;
-    RCHK(ensure_part_buffers(c, nsplit, set, c->even_nsplit));
+    const int rc0 = ensure_part_buffers(c, nsplit, set, c->even_nsplit);
+    if (rc0 == KNN_ERR_INVALID && c->pend) {
+        /* the pair's lists cannot grow under the pending step's: merge it
+         * alone first (as ctx_step_impl does) */
+        RCHK(merge_pending(c));
+        share = 0;
+        RCHK(ensure_part_buffers(c, nsplit, set, c->even_nsplit));
+    } else if (rc0) {
+        return rc0;
+    }
     hipStream_t cs = (hipStream_t)stream, ds = c->ds[ds_i];
     HIPCHK(hipEventRecord(c->ev_in, cs));
     HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
