@@ -429,8 +429,10 @@ __global__ __launch_bounds__(512) void k_dist_split(
 // the shared resource.  A 32x32x16 fragment feeds 16K multiply-adds: half
 // the LDS read bytes for the same work.
 //
-//   wave w: query group qg = w & 3 (32 queries), row half rh = w >> 2 (rows
-//   128 rh .. +127 of the 256-row tile, 4 m-blocks of 32); lane l = 32 h + r
+//   wave w: query group qg = w & 3 (32 queries), row half rh = w >> 2: the
+//   tile's m-blocks 2 b + rh (rows 64 b + 32 rh .. +31, b < 4), alternating
+//   between the two waves so that a run of consecutive rows (a cluster
+//   stored together) splits over both waves' lanes; lane l = 32 h + r
 //   supplies A row r / B query r with halves [8h, 8h + 8) of each 16-feature
 //   K-step -- 16-byte segments h, 2 + h (hi) and 4 + h, 6 + h (lo) of the
 //   128-byte chunk row; D register i of m-block b is row 32 b + 8 (i >> 2) +
@@ -554,7 +556,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
         const int u = 64 * wave_s + lane;
         const int p = ES == 8 ? u >> 1 : u;
         const int prh = p >> 7, ph = (p >> 6) & 1, pb = (p >> 4) & 3, pj = (p >> 2) & 3, pi = p & 3;
-        int row = (ts - cb.t0[bk]) * SP_TC + 128 * prh + 32 * pb + 8 * pj + 4 * ph + pi;
+        int row = (ts - cb.t0[bk]) * SP_TC + 64 * pb + 32 * prh + 8 * pj + 4 * ph + pi;
         row = row < cb.lim[bk] ? row : cb.lim[bk] - 1;
         const char *src = (const char *)((const T *)cb.nrm[bk] + row) + (ES == 8 ? (u & 1) * 4 : 0);
         glds4(src, (unsigned)(uintptr_t)lds + SP_NORM_OFF + (unsigned)(t & 3) * SP_NORM_SLOT +
@@ -567,9 +569,10 @@ __global__ __launch_bounds__(512) void k_dist_split32(
         const int eb = blk_of(t);
         const long c_base = cb.base[eb];
         const int nc = cb.nc[eb];
-        const int row0 = (t - cb.t0[eb]) * SP_TC + 128 * rh;        // the wave's first row
-        const long gt0 = (long)c_base + row0, gw0 = (long)q_base + qrow0 + 32 * qg;
-        const bool masked = (row0 + 128 > nc) || (gw0 < gt0 + 128 && gt0 < gw0 + 32);
+        const int tr0 = (t - cb.t0[eb]) * SP_TC;                    // the tile's first row
+        const int row0 = tr0 + 32 * rh;                              // the wave's m-block 0
+        const long gt0 = (long)c_base + tr0, gw0 = (long)q_base + qrow0 + 32 * qg;
+        const bool masked = (tr0 + SP_TC > nc) || (gw0 < gt0 + SP_TC && gt0 < gw0 + 32);
 #pragma unroll
         for (int b = 0; b < 4; b++)
 #pragma unroll
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
         const bool any = masked || __ballot(lanemin <= lim) != 0ull;
         if (any) {
             const float zfloor = (mode == KNN_MODE_INT) ? 0.f : -__builtin_inff();
-            // bit 16 b + i: row 32 b + 8 (i >> 2) + 4 h + (i & 3), rising with the bit
+            // bit 16 b + i: row 64 b + 8 (i >> 2) + 4 h + (i & 3) (+ row0), rising with the bit
             unsigned long long pend = 0;
 #pragma unroll
             for (int b = 0; b < 4; b++)
@@ -606,7 +609,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
                 for (int b = 0; b < 4; b++)
 #pragma unroll
                     for (int i = 0; i < 16; i++) {
-                        const int row = row0 + 32 * b + 8 * (i >> 2) + 4 * h + (i & 3);
+                        const int row = row0 + 64 * b + 8 * (i >> 2) + 4 * h + (i & 3);
                         if (!(row < nc && (long)c_base + row != gq)) pend &= ~(1ull << (16 * b + i));
                     }
             }
@@ -629,7 +632,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
                 const float dsel = b5 ? z1 : z0;
                 const float dd = (pend && dsel > zfloor) ? dsel : __builtin_inff();
                 const int i = bit & 15;
-                const int ii = (int)(c_base + row0 + 32 * (bit >> 4) + 8 * (i >> 2) + 4 * h + (i & 3));
+                const int ii = (int)(c_base + row0 + 64 * (bit >> 4) + 8 * (i >> 2) + 4 * h + (i & 3));
                 pend &= pend - 1;
                 list_insert<KL>(L, I, dd, ii);
             }
@@ -648,11 +651,11 @@ __global__ __launch_bounds__(512) void k_dist_split32(
         thr = fminf(thr, fminf(lmin, u));
     };
 
-    // fragment of segment s (0..7) of m-block b of the wave's row half
-    const int frow = 128 * rh + r32;                 // + 32 b: (R >> 1) & 7 does not depend on b
+    // fragment of segment s (0..7) of the wave's m-block b (tile rows 64 b + 32 rh + r)
+    const int frow = 32 * rh + r32;                  // + 64 b: (R >> 1) & 7 does not depend on b
     const int fsw = (frow >> 1) & 7;
     auto rdA = [&](const LDS_AS char *cs, int b, int sgm) {
-        return *(const LDS_AS knn_sh8 *)(cs + (frow + 32 * b) * 128 + 16 * (sgm ^ fsw));
+        return *(const LDS_AS knn_sh8 *)(cs + (frow + 64 * b) * 128 + 16 * (sgm ^ fsw));
     };
 
     if (total > 0) {
