@@ -429,20 +429,27 @@ __global__ __launch_bounds__(512) void k_dist_split(
 // the shared resource.  A 32x32x16 fragment feeds 16K multiply-adds: half
 // the LDS read bytes for the same work.
 //
-//   wave w: query group qg = w & 3 (32 queries), row half rh = w >> 2: the
-//   tile's m-blocks 2 b + rh (rows 64 b + 32 rh .. +31, b < 4), alternating
-//   between the two waves so that a run of consecutive rows (a cluster
-//   stored together) splits over both waves' lanes; lane l = 32 h + r
-//   supplies A row r / B query r with halves [8h, 8h + 8) of each 16-feature
-//   K-step -- 16-byte segments h, 2 + h (hi) and 4 + h, 6 + h (lo) of the
-//   128-byte chunk row; D register i of m-block b is row 32 b + 8 (i >> 2) +
-//   4 h + (i & 3) for query r.  A query's 4 lists: lanes h = 0, 1 of the two
+//   wave w: query group qg = w & 3 (32 queries), row half rh = w >> 2; lane
+//   l = 32 h + r supplies A row R = r / B query r with halves [8h, 8h + 8)
+//   of each 16-feature K-step -- 16-byte segments h, 2 + h (hi) and 4 + h,
+//   6 + h (lo) of the 128-byte chunk row.  A row R of the wave's m-block b
+//   (b < 4) is tile row 64 b + 16 (R >> 3) + 8 rh + (R & 7), so D register i
+//   of m-block b holds tile row 64 b + 16 (i >> 2) + 8 rh + 4 h + (i & 3)
+//   for query r: list 2 rh + h sees the rows 4 (2 rh + h) .. +3 mod 16, the
+//   same share as a lane group of the 16x16 form, so a run of consecutive
+//   rows (a cluster stored together) spreads evenly over the four lists.
+//   (Contiguous row halves a wave put 40 clustered rows on the two lanes of
+//   one wave, 20 a 16-entry list: 877 of 2050 queries of the near-tie test
+//   went uncertified; alternating 32-row m-blocks still left 31.)  A query's 4 lists: lanes h = 0, 1 of the two
 //   row-half waves (lpq = 4, list 2 rh + h); bounds shared by the two lanes
 //   of a wave.
-//   LDS image: segment s of tile row R at slot s ^ ((R >> 1) & 7) (the
-//   ds_read_b128 lane groups of a 32-row fragment read hit 16 distinct bank
-//   quads); norms ring [rh][h][b][j][i] (the lane's 64 rows contiguous).
+//   LDS image: segment s of tile row R at slot s ^ sw32(R), sw32(R) = bits
+//   1, 2, 4 of R (each 16-lane group of a fragment read -- rows 8 rh + 0..7
+//   and 16 + 8 rh + 0..7 of a 32-row group -- hits 16 distinct bank quads);
+//   norms ring [rh][h][b][j][i] (the lane's 64 rows contiguous).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ int sw32(int row) { return ((row >> 1) & 3) | ((row >> 2) & 4); }
+
 template <typename T, int KL>
 __global__ __launch_bounds__(512) void k_dist_split32(
     const char *__restrict__ qsp, const T *__restrict__ qnorm, size_t q_base, int nq,
@@ -516,7 +523,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
         const char *cp = s_row + (size_t)128 * s_fc;
         const int row = 32 * wave_s + 8 * i + lr;                   // tile row
         const int lrow = row < s_lim ? row : s_lim;
-        bglds16(knn_rsrc(cp), (unsigned)(lrow * rsb + 16 * (ls ^ ((row >> 1) & 7))),
+        bglds16(knn_rsrc(cp), (unsigned)(lrow * rsb + 16 * (ls ^ sw32(row))),
                 dst0 + (unsigned)(32 * wave_s + 8 * i) * 128u);
     };
     auto advance = [&]() {
@@ -556,7 +563,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
         const int u = 64 * wave_s + lane;
         const int p = ES == 8 ? u >> 1 : u;
         const int prh = p >> 7, ph = (p >> 6) & 1, pb = (p >> 4) & 3, pj = (p >> 2) & 3, pi = p & 3;
-        int row = (ts - cb.t0[bk]) * SP_TC + 64 * pb + 32 * prh + 8 * pj + 4 * ph + pi;
+        int row = (ts - cb.t0[bk]) * SP_TC + 64 * pb + 16 * pj + 8 * prh + 4 * ph + pi;
         row = row < cb.lim[bk] ? row : cb.lim[bk] - 1;
         const char *src = (const char *)((const T *)cb.nrm[bk] + row) + (ES == 8 ? (u & 1) * 4 : 0);
         glds4(src, (unsigned)(uintptr_t)lds + SP_NORM_OFF + (unsigned)(t & 3) * SP_NORM_SLOT +
@@ -570,7 +577,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
         const long c_base = cb.base[eb];
         const int nc = cb.nc[eb];
         const int tr0 = (t - cb.t0[eb]) * SP_TC;                    // the tile's first row
-        const int row0 = tr0 + 32 * rh;                              // the wave's m-block 0
+        const int row0 = tr0 + 8 * rh;                               // the wave's first row
         const long gt0 = (long)c_base + tr0, gw0 = (long)q_base + qrow0 + 32 * qg;
         const bool masked = (tr0 + SP_TC > nc) || (gw0 < gt0 + SP_TC && gt0 < gw0 + 32);
 #pragma unroll
@@ -598,7 +605,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
         const bool any = masked || __ballot(lanemin <= lim) != 0ull;
         if (any) {
             const float zfloor = (mode == KNN_MODE_INT) ? 0.f : -__builtin_inff();
-            // bit 16 b + i: row 64 b + 8 (i >> 2) + 4 h + (i & 3) (+ row0), rising with the bit
+            // bit 16 b + i: row 64 b + 16 (i >> 2) + 4 h + (i & 3) (+ row0), rising with the bit
             unsigned long long pend = 0;
 #pragma unroll
             for (int b = 0; b < 4; b++)
@@ -609,7 +616,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
                 for (int b = 0; b < 4; b++)
 #pragma unroll
                     for (int i = 0; i < 16; i++) {
-                        const int row = row0 + 64 * b + 8 * (i >> 2) + 4 * h + (i & 3);
+                        const int row = row0 + 64 * b + 16 * (i >> 2) + 4 * h + (i & 3);
                         if (!(row < nc && (long)c_base + row != gq)) pend &= ~(1ull << (16 * b + i));
                     }
             }
@@ -632,7 +639,7 @@ __global__ __launch_bounds__(512) void k_dist_split32(
                 const float dsel = b5 ? z1 : z0;
                 const float dd = (pend && dsel > zfloor) ? dsel : __builtin_inff();
                 const int i = bit & 15;
-                const int ii = (int)(c_base + row0 + 64 * (bit >> 4) + 8 * (i >> 2) + 4 * h + (i & 3));
+                const int ii = (int)(c_base + row0 + 64 * (bit >> 4) + 16 * (i >> 2) + 4 * h + (i & 3));
                 pend &= pend - 1;
                 list_insert<KL>(L, I, dd, ii);
             }
@@ -651,9 +658,9 @@ __global__ __launch_bounds__(512) void k_dist_split32(
         thr = fminf(thr, fminf(lmin, u));
     };
 
-    // fragment of segment s (0..7) of the wave's m-block b (tile rows 64 b + 32 rh + r)
-    const int frow = 32 * rh + r32;                  // + 64 b: (R >> 1) & 7 does not depend on b
-    const int fsw = (frow >> 1) & 7;
+    // fragment of segment s (0..7) of the wave's m-block b (tile row 64 b + frow)
+    const int frow = 16 * (r32 >> 3) + 8 * rh + (r32 & 7);   // sw32 does not depend on b
+    const int fsw = sw32(frow);
     auto rdA = [&](const LDS_AS char *cs, int b, int sgm) {
         return *(const LDS_AS knn_sh8 *)(cs + (frow + 64 * b) * 128 + 16 * (sgm ^ fsw));
     };
