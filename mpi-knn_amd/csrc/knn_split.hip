@@ -18,10 +18,11 @@
 //   tile = 256 corpus rows = 16 m-tiles of 16; a wave computes its 16
 //   queries against all 16 m-tiles (64 fp32 accumulators a lane);
 //   chunk = 128 bytes of every row (32 features: 32 hi then 32 lo halves);
-//   LDS stage = 32 KiB of corpus rows + 16 KiB of query rows, 3 stages
-//   filled by LDS-DMA (each wave stages its own 2 m-tiles and its own 16
-//   queries: 6 `buffer_load_dwordx4 ... lds` a chunk), a ring of 4 norm
-//   slices (256 norms each) two tiles ahead.
+//   LDS stage = 32 KiB of corpus rows, 4 stages filled by LDS-DMA (each
+//   wave stages its own 2 m-tiles: 4 `buffer_load_dwordx4 ... lds` a
+//   chunk), a ring of 4 norm slices (256 norms each) two tiles ahead; the
+//   query B fragments go straight to registers (global_load_dwordx4, one
+//   chunk ahead: a wave's queries are read by no other wave), 136 KiB.
 //
 // Accumulation (the error bound knn_cert_E(split) assumes exactly this):
 // a chunk's 96 products are summed apart -- three MFMAs into a zeroed fp32
@@ -767,8 +768,10 @@ static int launch_split(const void *qsp, const T *qnorm, size_t q_base, int nq, 
     const int rsb = (int)knn_split_rs((size_t)n);
     const int nqb = (nq + SP_TQ - 1) / SP_TQ;
     const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
-    const char *e16 = getenv("KNN_SPLIT16");
-    if (KL <= 24 && !(e16 && e16[0] == '1'))
+    // k_dist_split32 is opt-in (KNN_SPLIT32=1): mnist-real 21.7 ms a launch
+    // against the 16x16 form's 17.0 (tools/r05_s11.sh)
+    const char *e32 = getenv("KNN_SPLIT32");
+    if (KL <= 24 && e32 && e32[0] == '1')
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_split32<T, KL <= 24 ? KL : 24>), dim3((unsigned)(nqb_grid * nsplit)),
                            dim3(512), 0, s, (const char *)qsp, qnorm, q_base, nq, cb, n, rsb, nsplit, nqb, meta,
                            part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj, xord, m2s);
