@@ -147,10 +147,12 @@ def main():
                 eng.ctx.step_shadow_n([b.data_ptr() for b in sbufs[1:]], [r for _, r in blocks[1:]],
                                       [bs for bs, _ in blocks[1:]], eng.stream())
             elif efuse == "rest":
-                eng.step(bufs[0], blocks[0][1], blocks[0][0])
+                # the own block as ring.py folds it: the engine's own query
+                # block (the fused step then shares the own step's merge)
+                eng.step(eng.qb, blocks[0][1], blocks[0][0])
                 eng.step_n(bufs[1:], [r for _, r in blocks[1:]], [bs for bs, _ in blocks[1:]])
             elif efuse == "all":
-                eng.step_n(bufs, [r for _, r in blocks], [bs for bs, _ in blocks])
+                eng.step_n([eng.qb] + bufs[1:], [r for _, r in blocks], [bs for bs, _ in blocks])
             else:
                 for b, (base, rows) in enumerate(blocks):
                     if shadow:
