@@ -246,6 +246,17 @@ KNN_API size_t knn_shadow_norm_offset(size_t cap, size_t n);
 KNN_API int knn_shadow_pack(void *d_sblock, const void *d_block, size_t cap, size_t n, int dtype,
                             void *stream);
 
+/* Split fp16 rows of a packed block (the split-fp16 filter's form of
+ * real-valued data): for rows_pad(cap) rows, per 32 features the 32 halves
+ * hi = RN16(RN32(scale x)) then the 32 halves lo = RN16(RN32(scale x -
+ * hi)), zero past n; rows of round_up(n, 32) * 4 bytes (knn_split_bytes).
+ * scale: a power of two.  The engine converts the blocks of a split-filter
+ * search itself; this entry point exposes the same conversion for tests
+ * and tools. */
+KNN_API size_t knn_split_bytes(size_t cap, size_t n);
+KNN_API int knn_split_pack(void *d_dst, const void *d_block, size_t cap, size_t n, int dtype, double scale,
+                           void *stream);
+
 /* Pack rows (<= cap) points from a device source.  layout KNN_COLMAJOR:
  * element (i, j) at d_src[i + j*ld] (ld >= rows; the .mat layout,
  * serial:82); KNN_ROWMAJOR: d_src[i*ld + j] (ld >= n; blk:81-109).

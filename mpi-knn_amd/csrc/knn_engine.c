@@ -232,6 +232,16 @@ size_t knn_shadow_bytes(size_t cap, size_t n, int dtype)
                         KNN_META_DOUBLES * sizeof(double), 16);
 }
 
+size_t knn_split_bytes(size_t cap, size_t n) { return knn_rows_pad(cap) * knn_split_rs(n); }
+
+int knn_split_pack(void *d_dst, const void *d_block, size_t cap, size_t n, int dtype, double scale, void *stream)
+{
+    if (!d_dst || !d_block || !dtype_ok(dtype) || n == 0 || cap == 0 || !(scale > 0.0)) return KNN_ERR_INVALID;
+    int e = 0;
+    if (frexp(scale, &e) != 0.5) return KNN_ERR_INVALID;   /* a power of two */
+    return knn_launch_shadow_split(d_dst, d_block, dtype, knn_rows_pad(cap), n, (float)scale, stream);
+}
+
 int knn_shadow_pack(void *d_sblock, const void *d_block, size_t cap, size_t n, int dtype, void *stream)
 {
     if (!d_sblock || !d_block || !dtype_ok(dtype)) return KNN_ERR_INVALID;
@@ -1386,9 +1396,16 @@ static int ctx_step_split_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks
     memset(&tab, 0, sizeof(tab));
     memset(&mb, 0, sizeof(mb));
     tab.nblk = mb.nblk = nblk;
+    /* the blocks' split rows in one conversion launch */
+    void *cdst[KNN_SPLIT_MAXBLK];
+    size_t crows[KNN_SPLIT_MAXBLK];
     for (int b = 0; b < nblk; b++) {
-        char *sp = (char *)c->cspm[set] + per * (size_t)b;
-        RCHK(knn_launch_shadow_split(sp, d_cblocks[b], c->dtype, knn_rows_pad(nc[b]), c->n, c->sscale, ds));
+        cdst[b] = (char *)c->cspm[set] + per * (size_t)b;
+        crows[b] = knn_rows_pad(nc[b]);
+    }
+    RCHK(knn_launch_shadow_split_n(nblk, cdst, d_cblocks, crows, c->dtype, c->n, c->sscale, ds));
+    for (int b = 0; b < nblk; b++) {
+        char *sp = (char *)cdst[b];
         tab.sp[b] = sp;
         tab.nrm[b] = (const char *)d_cblocks[b] + norm_off;
         tab.base[b] = mb.base[b] = (int64_t)c_base[b];

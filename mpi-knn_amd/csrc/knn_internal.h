@@ -211,6 +211,9 @@ int knn_launch_begin_init(double *qthr, unsigned long long *qsum, int nq_pad, in
 static inline size_t knn_split_rs(size_t n) { return knn_round_up(n ? n : 1, 32) * 4; }
 int knn_launch_shadow_split(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n, float S,
                             void *stream);
+/* the same for nblk <= KNN_SPLIT_MAXBLK blocks in one launch */
+int knn_launch_shadow_split_n(int nblk, void *const *dst, const void *const *src, const size_t *rows_pad,
+                              int dtype, size_t n, float S, void *stream);
 /* knn_i8.hip: element block -> byte block (meta = the reduced meta) and the
  * int8 distance + top-k kernel (partial lists [split][query][2][kl]) */
 int knn_launch_shadow8(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,

@@ -2209,50 +2209,87 @@ extern "C" int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t r
     return hip_status();
 }
 
-// Split fp16 shadow rows (the H16 == 3 filter) of an fp32 block: per row and
-// 32-feature group, the 32 halves hi = RN16(S x) then the 32 halves lo =
-// RN16(S x - hi) (S x - hi is exact in fp32: Sterbenz); zero past n.  One
-// thread per 8 features: a 16-byte hi and a 16-byte lo store.
+// Split fp16 shadow rows (the split filter) of fp32 / fp64 blocks: per row
+// and 32-feature group, the 32 halves hi = RN16(S x) then the 32 halves lo =
+// RN16(S x - hi) (S x - hi is exact in fp32: Sterbenz; fp64: exact in fp64,
+// rounded once to fp16 through fp32); zero past n.  One thread per 16 bytes
+// of source row (V = 2 fp64 / 4 fp32 features): a wave reads 1 KiB of a row
+// contiguously and its 16-lane groups write whole 64-byte hi and lo runs.
+// (Round 4's form, one thread per 8 features with 8-byte loads 64 bytes
+// apart, moved a 7552 x 784 fp64 block in 35 us, 2 TB/s.)  Up to
+// KNN_SPLIT_MAXBLK blocks per launch (a ring rank's received blocks).
+struct knn_split_conv_t {
+    char *dst[KNN_SPLIT_MAXBLK];
+    const void *src[KNN_SPLIT_MAXBLK];
+    long long i0[KNN_SPLIT_MAXBLK + 1];   // first flat work item of block b
+    int nblk;
+};
+
 template <typename T>
-__global__ __launch_bounds__(256) void k_shadow_split(char *__restrict__ dst, const T *__restrict__ src,
-                                                      size_t rows, int n, int nps, int npd, float S)
+__global__ __launch_bounds__(256) void k_shadow_split(const knn_split_conv_t cv, int n, int nps, int npd, float S)
 {
-    const size_t per = (size_t)npd / 8, tot = rows * per;
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < tot; i += (size_t)gridDim.x * 256) {
-        const size_t r = i / per;
-        const int j0 = (int)(i - r * per) * 8;
-        const T *row = src + r * (size_t)nps;
-        knn_h8 hi, lo;
+    constexpr int V = 16 / (int)sizeof(T);
+    typedef typename std::conditional<sizeof(T) == 8, dbl2, flt4>::type vec_t;
+    typedef _Float16 hv_t __attribute__((ext_vector_type(V)));
+    const int per = npd / V;   // work items a row
+    const long long tot = cv.i0[cv.nblk];
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < tot; i += (long long)gridDim.x * 256) {
+        int b = 0;
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            // fp64: x S - hi exact in fp64, rounded once to fp16 (through
-            // fp32: exact, |x S - hi| has <= 24 significant bits below hi's)
-            const T x = j0 + e < n ? row[j0 + e] * (T)S : (T)0;
+        for (int x = 1; x < KNN_SPLIT_MAXBLK; x++) b = (x < cv.nblk && i >= cv.i0[x]) ? x : b;
+        const long long li = i - cv.i0[b];
+        const long long r = li / per;
+        const int j0 = (int)(li - r * per) * V;
+        vec_t v{};
+        if (j0 < n) v = *(const vec_t *)((const T *)cv.src[b] + r * (long long)nps + j0);
+        hv_t hi, lo;
+#pragma unroll
+        for (int e = 0; e < V; e++) {
+            const T x = (j0 + e < n) ? v[e] * (T)S : (T)0;
             const _Float16 h = (_Float16)(float)x;
             hi[e] = h;
             lo[e] = (_Float16)(float)(x - (T)(float)h);
         }
-        char *o = dst + r * (size_t)npd * 4 + (size_t)(j0 >> 5) * 128 + 2 * (j0 & 31);
-        *(knn_h8 *)o = hi;
-        *(knn_h8 *)(o + 64) = lo;
+        char *o = cv.dst[b] + r * (long long)npd * 4 + (long long)(j0 >> 5) * 128 + 2 * (j0 & 31);
+        *(hv_t *)o = hi;
+        *(hv_t *)(o + 64) = lo;
     }
+}
+
+// nblk blocks: dst[b] <- split rows of src[b] (rows_pad[b] rows each)
+extern "C" int knn_launch_shadow_split_n(int nblk, void *const *dst, const void *const *src, const size_t *rows_pad,
+                                         int dtype, size_t n, float S, void *stream)
+{
+    if (nblk < 1 || nblk > KNN_SPLIT_MAXBLK || n == 0) return KNN_ERR_INVALID;
+    const int npd = (int)knn_round_up(n, 32), nps = (int)knn_n_pad_dt(n, dtype);
+    const int V = dtype == KNN_F64 ? 2 : 4;
+    knn_split_conv_t cv{};
+    cv.nblk = nblk;
+    cv.i0[0] = 0;
+    for (int b = 0; b < nblk; b++) {
+        if (!dst[b] || !src[b]) return KNN_ERR_INVALID;
+        cv.dst[b] = (char *)dst[b];
+        cv.src[b] = src[b];
+        cv.i0[b + 1] = cv.i0[b] + (long long)rows_pad[b] * (npd / V);
+    }
+    for (int b = nblk + 1; b <= KNN_SPLIT_MAXBLK; b++) cv.i0[b] = cv.i0[nblk];
+    const long long tot = cv.i0[nblk];
+    const unsigned grid = (unsigned)(tot / 256 + 1 < 16384 ? tot / 256 + 1 : 16384);
+    if (dtype == KNN_F32)
+        hipLaunchKernelGGL(k_shadow_split<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, cv, (int)n, nps,
+                           npd, S);
+    else if (dtype == KNN_F64)
+        hipLaunchKernelGGL(k_shadow_split<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream, cv, (int)n, nps,
+                           npd, S);
+    else
+        return KNN_ERR_INVALID;
+    return hip_status();
 }
 
 extern "C" int knn_launch_shadow_split(void *dst, const void *blk, int dtype, size_t rows_pad, size_t n,
                                        float S, void *stream)
 {
-    const int npd = (int)knn_round_up(n, 32), nps = (int)knn_n_pad_dt(n, dtype);
-    const size_t tot = rows_pad * (size_t)npd / 8;
-    const unsigned grid = (unsigned)(tot / 256 + 1 < 8192 ? tot / 256 + 1 : 8192);
-    if (dtype == KNN_F32)
-        hipLaunchKernelGGL(k_shadow_split<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char *)dst,
-                           (const float *)blk, rows_pad, (int)n, nps, npd, S);
-    else if (dtype == KNN_F64)
-        hipLaunchKernelGGL(k_shadow_split<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char *)dst,
-                           (const double *)blk, rows_pad, (int)n, nps, npd, S);
-    else
-        return KNN_ERR_INVALID;
-    return hip_status();
+    return knn_launch_shadow_split_n(1, &dst, &blk, &rows_pad, dtype, n, S, stream);
 }
 
 extern "C" int knn_launch_wire(int unpack, void *dst, const void *src, int dtype, size_t cnt,

@@ -44,7 +44,7 @@ API_SYMBOLS = (
     "knn_ctx_profile", "knn_block_bytes_dt", "knn_block_meta_offset_dt", "knn_block_pack_dt",
     "knn_ctx_create_dt", "knn_classify_device", "knn_search_mpi_compat",
     "knn_ctx_contraction_bits", "knn_wire_bytes", "knn_wire_ok", "knn_wire_pack",
-    "knn_wire_unpack", "knn_shadow_bytes", "knn_shadow_norm_offset", "knn_shadow_pack",
+    "knn_wire_unpack", "knn_shadow_bytes", "knn_shadow_norm_offset", "knn_shadow_pack", "knn_split_bytes", "knn_split_pack",
     "knn_ctx_shadow", "knn_ctx_step_shadow", "knn_ctx_begin_meta", "knn_ctx_shadow_bytes",
     "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n", "knn_ctx_split", "knn_s8_block_bytes",
     "knn_s8_block_meta_offset", "knn_block_pack_s8", "knn_s8_spec_ok", "knn_ctx_begin_s8",
@@ -118,6 +118,8 @@ def _load():
         "knn_shadow_bytes": ([sz, sz, i], sz),
         "knn_shadow_norm_offset": ([sz, sz], sz),
         "knn_shadow_pack": ([p, p, sz, sz, i, p], i),
+        "knn_split_bytes": ([sz, sz], sz),
+        "knn_split_pack": ([p, p, sz, sz, i, ctypes.c_double, p], i),
         "knn_ctx_shadow": ([p], i),
         "knn_ctx_step_shadow": ([p, p, sz, sz, p], i),
         "knn_ctx_step_shadow_n": ([p, i, pp, psz, psz, p], i),
@@ -280,6 +282,15 @@ def shadow_bytes(cap, n, dtype="f64"):
 def shadow_pack(d_sblock, d_block, cap, n, dtype="f64", stream=0):
     _check(lib.knn_shadow_pack(d_sblock, d_block, cap, n, DTYPES[dtype], stream or None),
            "knn_shadow_pack")
+
+
+def split_bytes(cap, n):
+    return lib.knn_split_bytes(cap, n)
+
+
+def split_pack(d_dst, d_block, cap, n, dtype="f64", scale=1.0, stream=0):
+    _check(lib.knn_split_pack(d_dst, d_block, cap, n, DTYPES[dtype], float(scale), stream or None),
+           "knn_split_pack")
 
 
 def block_pack(d_block, cap, rows, n, d_src, ld, layout, stream=0, dtype="f64", src_dtype="f64"):
