@@ -248,8 +248,8 @@ KNN_API int knn_shadow_pack(void *d_sblock, const void *d_block, size_t cap, siz
 
 /* Split fp16 rows of a packed block (the split-fp16 filter's form of
  * real-valued data): for rows_pad(cap) rows, per 32 features the 32 halves
- * hi = RN16(RN32(scale x)) then the 32 halves lo = RN16(RN32(scale x -
- * hi)), zero past n; rows of round_up(n, 32) * 4 bytes (knn_split_bytes).
+ * hi = RN16(scale x) then the 32 halves lo = RN16(scale x - hi), each
+ * rounded once from the block's precision, zero past n; rows of round_up(n, 32) * 4 bytes (knn_split_bytes).
  * scale: a power of two.  The engine converts the blocks of a split-filter
  * search itself; this entry point exposes the same conversion for tests
  * and tools. */

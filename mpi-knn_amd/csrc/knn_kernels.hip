@@ -2211,8 +2211,8 @@ extern "C" int knn_launch_shadow(void *dst, const void *blk, int dtype, size_t r
 
 // Split fp16 shadow rows (the split filter) of fp32 / fp64 blocks: per row
 // and 32-feature group, the 32 halves hi = RN16(S x) then the 32 halves lo =
-// RN16(S x - hi) (S x - hi is exact in fp32: Sterbenz; fp64: exact in fp64,
-// rounded once to fp16 through fp32); zero past n.  One thread per 16 bytes
+// RN16(S x - hi), each rounded once from the block's precision (S x - hi is
+// exact there: Sterbenz); zero past n.  One thread per 16 bytes
 // of source row (V = 2 fp64 / 4 fp32 features): a wave reads 1 KiB of a row
 // contiguously and its 16-lane groups write whole 64-byte hi and lo runs.
 // (Round 4's form, one thread per 8 features with 8-byte loads 64 bytes
@@ -2245,10 +2245,13 @@ __global__ __launch_bounds__(256) void k_shadow_split(const knn_split_conv_t cv,
         hv_t hi, lo;
 #pragma unroll
         for (int e = 0; e < V; e++) {
+            // one rounding each, from the block's precision (x - hi is exact
+            // in it: Sterbenz).  (Written as conversions through fp32, the
+            // compiler folds them into these single roundings anyway.)
             const T x = (j0 + e < n) ? v[e] * (T)S : (T)0;
-            const _Float16 h = (_Float16)(float)x;
+            const _Float16 h = (_Float16)x;
             hi[e] = h;
-            lo[e] = (_Float16)(float)(x - (T)(float)h);
+            lo[e] = (_Float16)(x - (T)h);
         }
         char *o = cv.dst[b] + r * (long long)npd * 4 + (long long)(j0 >> 5) * 128 + 2 * (j0 & 31);
         *(hv_t *)o = hi;

@@ -6,7 +6,8 @@ is subnormal or zero, and several scales.
 
 Restatement (the filter's representation, knn_kernels.hip k_shadow_split):
 x = scale * v in the block's precision (scale a power of two: exact), hi =
-RN16(RN32(x)), lo = RN16(RN32(x - hi)); per row and 32-feature group the 32
+RN16(x), lo = RN16(x - hi), each rounded once from that precision (numpy's
+float64 -> float16 conversion rounds once; x - hi is exact); per row and 32-feature group the 32
 hi halves then the 32 lo halves; zero past n.  This is the product's own
 representation, not the reference's arithmetic (the reference's S is
 recomputed exactly in k_merge), so a numpy restatement is its oracle.
@@ -20,8 +21,8 @@ pytestmark = pytest.mark.gpu
 def split_rows(V, n, scale, dt):
     T = np.float64 if dt == "f64" else np.float32
     x = V.astype(T) * T(scale)
-    hi = x.astype(np.float32).astype(np.float16)
-    lo = (x - hi.astype(np.float32).astype(T)).astype(np.float32).astype(np.float16)
+    hi = x.astype(np.float16)
+    lo = (x - hi.astype(T)).astype(np.float16)
     m = V.shape[0]
     npd = (n + 31) // 32 * 32
     H = np.zeros((m, npd), np.float16)
