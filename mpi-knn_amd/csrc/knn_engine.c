@@ -90,6 +90,9 @@ struct knn_ctx {
     int *st_i;
     /* unresolved queries */
     int *fail_count, *fail_list, *mode_dev;
+    /* the pair's host copy (pinned, mapped): k_count_out writes it behind
+     * the last merge, so knn_ctx_end's read-back is no blit */
+    int *h_count, *h_count_dev;
     double *fbound;     /* per query: rescan bound on the k-th key (k_finalize) */
     double *rs_d;
     int *rs_i;
@@ -328,6 +331,7 @@ static void ctx_free_buffers(knn_ctx_t *c)
     hipFree(c->st_T);
     hipFree(c->st_i);
     hipFree(c->fail_count);
+    if (c->h_count) hipHostFree(c->h_count);
     hipFree(c->fail_list);
     hipFree(c->fbound);
     hipFree(c->rs_d);
@@ -445,6 +449,8 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     ok &= hipMalloc((void **)&c->fail_list, np * sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->fbound, np * sizeof(double)) == hipSuccess;
     if (ok) c->mode_dev = c->fail_count + 1;
+    ok &= hipHostMalloc((void **)&c->h_count, 2 * sizeof(int), hipHostMallocMapped) == hipSuccess;
+    ok &= c->h_count && hipHostGetDevicePointer((void **)&c->h_count_dev, c->h_count, 0) == hipSuccess;
     for (int b = 0; b < 2; b++) {
         ok &= hipStreamCreateWithFlags(&c->ds[b], hipStreamNonBlocking) == hipSuccess;
         ok &= hipEventCreateWithFlags(&c->ev_d[b], hipEventDisableTiming) == hipSuccess;
@@ -1687,14 +1693,15 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
                                  (int)c->nq, (int)c->n, c->k, c->meta, d_out, c->fail_count,
                                  c->fail_list, c->mode_dev, c->fbound, env_on("KNN_FORCE_RESCAN"),
                                  c->split, c->ms));
-    int host[2];
-    HIPCHK(hipMemcpyAsync(host, c->fail_count, 2 * sizeof(int), hipMemcpyDeviceToHost, c->ms));
+    c->h_count[0] = c->h_count[1] = -1;
+    RCHK(knn_launch_count_out(c->fail_count, c->h_count_dev, c->ms));
     HIPCHK(hipEventRecord(c->ev_end, c->ms));
     HIPCHK(hipStreamWaitEvent(s, c->ev_end, 0));
     HIPCHK(hipStreamSynchronize(c->ms));
     RCHK(prof_collect(c));
-    c->nfail = host[0];
-    c->mode = host[1];
+    c->nfail = ((volatile int *)c->h_count)[0];
+    c->mode = ((volatile int *)c->h_count)[1];
+    if (c->nfail < 0) return KNN_ERR_HIP;
     if (c->nfail > 0 && research8(c, d_out, s) != KNN_OK) {
         /* the re-search is an optimisation: on any failure of it the exact
          * rescan resolves the same queries.  The rescan reads only the host

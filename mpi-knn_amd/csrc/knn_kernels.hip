@@ -1993,6 +1993,19 @@ __global__ void k_begin_init(double *qthr, unsigned long long *qsum, int nq_pad,
     if (i < 2) counts[i] = 0;
 }
 
+// the search's (unresolved, mode) pair into mapped host memory (knn_ctx_end
+// reads it after synchronising with the stream)
+__global__ void k_count_out(const int *__restrict__ src, int *__restrict__ dst)
+{
+    if (threadIdx.x < 2) dst[threadIdx.x] = src[threadIdx.x];
+}
+
+extern "C" int knn_launch_count_out(const int *d_count, int *mapped, void *stream)
+{
+    hipLaunchKernelGGL(k_count_out, dim3(1), dim3(64), 0, (hipStream_t)stream, d_count, mapped);
+    return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
+}
+
 extern "C" int knn_launch_begin_init(double *qthr, unsigned long long *qsum, int nq_pad, int *counts,
                                      void *stream)
 {
