@@ -1139,7 +1139,14 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     HIPCHK(hipSetDevice(c->device));
     RCHK(flush_pend2(c, NULL, NULL));   /* a deferred merge goes first, in step order */
     c->split_solo = c->i8 && c->nstep == 0 && !xb && d_sblock != NULL && d_sblock == c->q8 && nc == c->nq;
-    const int nsplit = choose_splits(c, nc);
+    int nsplit = choose_splits(c, nc);
+    {
+        /* (diagnostic: the split count of a split-filter search's own-block
+         * step, whose merge the fused step shares) */
+        const char *os_ = getenv("KNN_OWN_SPLITS");
+        if (os_ && atoi(os_) > 0 && c->split && !xb && c->nstep == 0 && d_cblock == c->qblk)
+            nsplit = atoi(os_) < KNN_MAX_LISTS / c->lpq ? atoi(os_) : KNN_MAX_LISTS / c->lpq;
+    }
     const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
     c->nsplit_last = nsplit;
     /* pairing: in exact-integer (fp16) searches two consecutive steps share
