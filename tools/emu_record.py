@@ -3,7 +3,9 @@
 written by `tools/gpu.sh emu:WL[:RANKS[:STEPS]]`) into
 profiles/<tag>_ring_emulation.json.
 
-  python tools/emu_record.py r02 "note text"
+  python tools/emu_record.py r02 "note text" [LOGDIR]
+
+LOGDIR (default gpurun_out): where the emu_<workload>.log files are.
 """
 import glob
 import json
@@ -24,7 +26,8 @@ def last_json(path):
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
     out = {}
-    for f in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "emu_*.log"))):
+    logdir = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "gpurun_out")
+    for f in sorted(glob.glob(os.path.join(logdir, "emu_*.log"))):
         rec = last_json(f)
         if rec and "workload" in rec:
             out[rec["workload"]] = rec
