@@ -68,6 +68,9 @@ typedef _Float16 knn_sh8 __attribute__((ext_vector_type(8)));
 #ifndef SP_ABL_NODMA
 #define SP_ABL_NODMA 0
 #endif
+#ifndef SP_NOPRE   /* (diagnostic: no next-chunk fragment prefetch) */
+#define SP_NOPRE 0
+#endif
 
 // fp64 bound -> fp32 bound rounded up (still a bound: a candidate above it
 // is above the fp64 one)
@@ -335,14 +338,25 @@ __global__ __launch_bounds__(512) void k_dist_split(
         __builtin_amdgcn_s_barrier();
 
         int st = 0, fcq = 0;                          // stage / row chunk computed
+        // A fragments of the first D m-tiles: read at the chunk's start, or
+        // -- for every chunk but a tile's first -- during the previous
+        // chunk's last D m-tiles.  The next chunk's stage is valid then: the
+        // barrier that ended the chunk before saw every wave's pieces of it
+        // land (vmcnt(4) leaves only the chunk three ahead in flight), and
+        // it is overwritten only after the barrier that ends the next chunk.
+        // Read at the start, the first fragments of all 8 waves queued behind
+        // one another right after the barrier while the MFMA pipes idled.
+        knn_sh8 ah[D], al[D];
         for (int t = t_lo; t < t_hi; t++) {
             gnorm(t + 2);
             for (int fc = 0; fc < nfc; fc++) {
                 LDS_AS char *cs = lds + st * SP_STAGE;
+                const bool pre = fc + 1 < nfc && !SP_ABL_NOFRAG && !SP_NOPRE;   // prefetch into the next chunk
+                LDS_AS char *cn_ = lds + (st == SP_NST - 1 ? 0 : st + 1) * SP_STAGE;
                 // next chunk's query fragments (the row's chunks cycle every tile)
                 fcq = fcq + 1 == nfc ? 0 : fcq + 1;
                 bload(fcq, qh_n, ql_n);
-                knn_sh8 qh, ql, ah[D], al[D];
+                knn_sh8 qh, ql;
                 if (SP_ABL_NOFRAG) {
                     qh = ql = (knn_sh8){1, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -350,10 +364,12 @@ __global__ __launch_bounds__(512) void k_dist_split(
                 } else {
                     qh = __builtin_bit_cast(knn_sh8, qh_c);
                     ql = __builtin_bit_cast(knn_sh8, ql_c);
+                    if (fc == 0 || SP_NOPRE) {
 #pragma unroll
-                    for (int d = 0; d < D; d++) {
-                        ah[d] = *(const LDS_AS knn_sh8 *)(cs + d * 2048 + fs0);
-                        al[d] = *(const LDS_AS knn_sh8 *)(cs + d * 2048 + fs1);
+                        for (int d = 0; d < D; d++) {
+                            ah[d] = *(const LDS_AS knn_sh8 *)(cs + d * 2048 + fs0);
+                            al[d] = *(const LDS_AS knn_sh8 *)(cs + d * 2048 + fs1);
+                        }
                     }
                 }
                 flt4 tt[2];
@@ -371,9 +387,13 @@ __global__ __launch_bounds__(512) void k_dist_split(
                         tt[mt & 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[sl], qh, x, 0, 0, 0);
                     }
                     // m-tile mt + D's fragments into the slot just consumed
+                    // (past the last m-tile: the next chunk's first ones)
                     if (mt + D < 16 && !SP_ABL_NOFRAG) {
                         ah[sl] = *(const LDS_AS knn_sh8 *)(cs + (mt + D) * 2048 + fs0);
                         al[sl] = *(const LDS_AS knn_sh8 *)(cs + (mt + D) * 2048 + fs1);
+                    } else if (mt + D >= 16 && pre) {
+                        ah[sl] = *(const LDS_AS knn_sh8 *)(cn_ + (mt + D - 16) * 2048 + fs0);
+                        al[sl] = *(const LDS_AS knn_sh8 *)(cn_ + (mt + D - 16) * 2048 + fs1);
                     }
                     if (mt > 0) acc[mt - 1] += tt[(mt - 1) & 1];
                     // chunk c + 3 into the stage chunk c - 1 left (freed by the
