@@ -1674,20 +1674,9 @@ static int ctx_end_device(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
     return KNN_OK;
 }
 
-int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *stream)
+/* knn_ctx_end's device part and count read-back, on stream c->ms */
+static int ctx_end_merge(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
 {
-    if (!c || !d_out || c->first_step) return KNN_ERR_INVALID;
-    HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = (hipStream_t)stream;
-    /* finalize and the counter read-back run on the merge stream right
-     * behind the last merge: every cross-stream wait (hipStreamWaitEvent)
-     * put ~20 us of latency on the pass's critical path, even when the
-     * event had long completed (rocprofv3 of the P = 8 ring emulation).
-     * The records go to d_out from the merge stream, so that stream first
-     * waits for the caller's stream as it stands now: d_out may have just
-     * been allocated, cleared or read there (a caching allocator hands out
-     * memory that pending work on the caller's stream used last).  The
-     * caller's stream is ordered after the results. */
     HIPCHK(hipEventRecord(c->ev_in, s));
     HIPCHK(hipStreamWaitEvent(c->ms, c->ev_in, 0));
     /* the last merge (deferred or pending) finalizes too when it is the
@@ -1705,6 +1694,34 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     HIPCHK(hipEventRecord(c->ev_end, c->ms));
     HIPCHK(hipStreamWaitEvent(s, c->ev_end, 0));
     HIPCHK(hipStreamSynchronize(c->ms));
+    return KNN_OK;
+}
+
+int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *stream)
+{
+    if (!c || !d_out || c->first_step) return KNN_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    /* The last merge, finalize and the counter read-back run behind the
+     * search's last distance launch: on the merge stream when earlier
+     * merges ran there (they update the state in step order), otherwise on
+     * that launch's own stream (after the other distance stream's last
+     * launch) -- every cross-stream hop put 20-30 us on the pass's critical
+     * path in the rocprofv3 traces (a P = 1 search: distance kernel ->
+     * 25 us -> merge on the merge stream).  The records go to d_out, so
+     * that stream first waits for the caller's stream as it stands now:
+     * d_out may have just been allocated, cleared or read there (a caching
+     * allocator hands out memory that pending work on the caller's stream
+     * used last).  The caller's stream is ordered after the results. */
+    hipStream_t ms = c->ms;
+    if (!c->merged && c->nstep >= 1 && !env_on("KNN_END_ON_MS")) {
+        const int last = (c->nstep - 1) & 1;
+        if (c->nstep >= 2) HIPCHK(hipStreamWaitEvent(c->ds[last], c->ev_d[last ^ 1], 0));
+        c->ms = c->ds[last];
+    }
+    const int rc_end = ctx_end_merge(c, d_out, s);
+    c->ms = ms;
+    RCHK(rc_end);
     RCHK(prof_collect(c));
     c->nfail = ((volatile int *)c->h_count)[0];
     c->mode = ((volatile int *)c->h_count)[1];
