@@ -1674,11 +1674,10 @@ static int ctx_end_device(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
     return KNN_OK;
 }
 
-/* knn_ctx_end's device part and count read-back, on stream c->ms */
+/* knn_ctx_end's device part and count read-back, on stream c->ms; the
+ * caller's stream has been waited for on the host (end_wait) */
 static int ctx_end_merge(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
 {
-    HIPCHK(hipEventRecord(c->ev_in, s));
-    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_in, 0));
     /* the last merge (deferred or pending) finalizes too when it is the
      * rank merge (INT-mode int8 lists) */
     int fin = 0;
@@ -1713,10 +1712,20 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
      * d_out may have just been allocated, cleared or read there (a caching
      * allocator hands out memory that pending work on the caller's stream
      * used last).  The caller's stream is ordered after the results. */
+    /* The orderings end() needs besides the last distance launch -- the
+     * caller's stream as it stands now, and the other distance stream's last
+     * launch -- are waited for on the HOST: end() blocks until the results
+     * anyway, both are normally complete long before the last launch, and a
+     * stream wait costs 20-25 us of GPU time on the queue even on an event
+     * that completed long before (rocprofv3, P = 1: distance kernel -> 24 us
+     * -> merge on the same queue, with only the caller-stream wait between).
+     * Nothing on the caller's stream can wait on work end() enqueues. */
+    HIPCHK(hipEventRecord(c->ev_in, s));
+    HIPCHK(hipEventSynchronize(c->ev_in));
     hipStream_t ms = c->ms;
     if (!c->merged && c->nstep >= 1 && !env_on("KNN_END_ON_MS")) {
         const int last = (c->nstep - 1) & 1;
-        if (c->nstep >= 2) HIPCHK(hipStreamWaitEvent(c->ds[last], c->ev_d[last ^ 1], 0));
+        if (c->nstep >= 2) HIPCHK(hipEventSynchronize(c->ev_d[last ^ 1]));
         c->ms = c->ds[last];
     }
     const int rc_end = ctx_end_merge(c, d_out, s);
