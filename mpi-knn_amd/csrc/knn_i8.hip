@@ -758,97 +758,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     };
 
     // ---- main loop -------------------------------------------------------------
-    // AL: A-fragment lead in K-steps.  2 on the half-tile kernel's long rows
-    // (one query group): the fragments of K-step k + 2 are read at K-step k,
-    // and the barrier that certifies chunk x + 1 moves to chunk x's start, so
-    // a read may reach one chunk ahead (two in the one place a tile's last
-    // chunk is a single K-step: there the next tile's first two K-steps are
-    // read together at that K-step).  With a lead of one K-step the reads
-    // were issued one MFMA pair before their use and the bare MFMA / ds_read
-    // loop ran at half the int8 peak.  (I8_AL1: the
-    // lead-1 form, for A/B builds.)
-#ifndef I8_AL1
-#define I8_AL1 0
-#endif
-    constexpr int AL = (TM == 2 && QG == 1 && !SHORT && NKS >= 8 && NKS <= 25 && !I8_AL1) ? 2 : 1;   // (28 K-steps: it spills)
-    if (AL == 2 && total > 0) {
-#pragma unroll
-        for (int y = 0; y < NST - 2; y++) stage();
-        wait_next();
-        __builtin_amdgcn_s_barrier();   // B(0)
-        knn_v4i a0[MB], a1[MB];         // K-steps 0 and 1 of the next tile, read ahead
-        rdA(0, 0, a0);
-        rdA(0, 1, a1);
-        stage();
-        constexpr int KT_LAST = NKS - 4 * (NCH - 1);
-        int x = 0;
-        e_b = i8_blk_of(tab, t_lo);
-        e_t0 = i8_rfl(tab->t0[e_b]);
-        e_t1 = i8_rfl(tab->t0[e_b + 1]);
-        c_base = (long)i8_rfl64(tab->base[e_b]);
-        nc = i8_rfl(tab->nc[e_b]);
-        for (int t = t_lo; t < t_hi; t++) {
-            if (t == e_t1) {   // the epilogue's block moves on
-                e_b++;
-                e_t0 = e_t1;
-                e_t1 = i8_rfl(tab->t0[e_b + 1]);
-                c_base = (long)i8_rfl64(tab->base[e_b]);
-                nc = i8_rfl(tab->nc[e_b]);
-            }
-            knn_v16i acc[QG][MB];
-#pragma unroll
-            for (int bb = 0; bb < MB; bb++)
-#pragma unroll
-                for (int i = 0; i < 16; i++) acc[0][bb][i] = 0;
-            // the tile's fragments, one set a K-step (fully unrolled: the
-            // compiler keeps the ~3 live sets in registers)
-            knn_v4i af[NKS][MB];
-#pragma unroll
-            for (int bb = 0; bb < MB; bb++) {
-                af[0][bb] = a0[bb];
-                af[1][bb] = a1[bb];
-            }
-            // ring chunk of the next tile's first chunk, from chunk c
-            const int xn0 = x + NCH;
-            const bool next = xn0 < total;
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                const int kt = NKS - 4 * c < 4 ? NKS - 4 * c : 4;
-                if (x + 1 < total) {
-                    wait_next();
-                    __builtin_amdgcn_s_barrier();   // B(x + 1): chunk x + 1 readable from here
-                    stage();
-                }
-#pragma unroll
-                for (int ks = 0; ks < 4; ks++) {
-                    if (ks < kt) {
-                        const int k = 4 * c + ks;
-                        if (k + 2 < NKS) {
-                            rdA(x + ((k + 2) >> 2) - c, (k + 2) & 3, af[k + 2]);
-                        } else if (next) {
-                            // the next tile's K-steps 0 and 1 (chunk x + NCH - c)
-                            if (KT_LAST >= 2 || c == NCH - 1) {
-                                if (k + 2 - NKS == 0 || (KT_LAST == 1 && c == NCH - 1)) rdA(xn0, 0, a0);
-                                if (k + 2 - NKS == 1 || (KT_LAST == 1 && c == NCH - 1)) rdA(xn0, 1, a1);
-                            }
-                        }
-                        // keep the reads ahead of this K-step's MFMAs (left
-                        // alone, the scheduler sinks them behind the MFMAs)
-                        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                        for (int bb = 0; bb < MB; bb++)
-                            acc[0][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[k][bb], qf[0][k], acc[0][bb], 0, 0, 0);
-                    }
-                }
-                x++;
-            }
-            epilogue(t, acc, x);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA left in flight
-        if constexpr (REREAD) {
-            if (q_ready >= 0) qthr_apply();
-        }
-    } else if (total > 0) {
+    if (total > 0) {
 #pragma unroll
         for (int y = 0; y < NST - 2; y++) stage();
         wait_next();
