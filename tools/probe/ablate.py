@@ -11,6 +11,8 @@ with  KB8_SO=tools/probe/abl/libkbench8_<name>.so python tools/probe/kbench8.py
   nodma        epilogue kept, staging removed (garbage keys: timing only)
   noepi_halfdma  one of each wave's two pieces a chunk (timing only)
   noepi_nowait   pieces issued, never waited for (racy: timing only)
+  stamp        the product kernel plus per-workgroup wall-clock stamps
+               (s_memrealtime at start, first chunk ready, loop done, end)
   count        the product kernel plus per-wave event counters (one vector
                atomic a wave and event, lane 0): groups past the init-word
                filter (all groups where it is off), groups whose exact keys
@@ -40,7 +42,29 @@ COUNT_HDR = """__device__ unsigned long long kb8_cnt[8];
 """
 
 
+STAMP_HDR = """__device__ unsigned long long kb8_stamp[4 * 16384];
+#define KB8_STAMP 1
+#define KB8S(i) do { if (threadIdx.x == 0 && blockIdx.x < 16384) \\
+    kb8_stamp[4 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+"""
+
+
 def patch(s, name):
+    if name == "stamp":
+        # per-workgroup wall clock (100 MHz): start, first chunk ready, loop
+        # done, end -- kbench8.py prints the spans of the last timed launch
+        s = STAMP_HDR + s
+        for old, new in (
+                ("    const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;\n",
+                 "    const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;\n    KB8S(0);\n"),
+                ("        rdA(0, 0, acur);\n", "        KB8S(1);\n        rdA(0, 0, acur);\n"),
+                ("        asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA left in flight\n",
+                 "        asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");   // no LDS-DMA left in flight\n        KB8S(2);\n"),
+                ("            atomicMin(qthr + myq[g], (unsigned long long)__double_as_longlong((double)thr[g]));\n    }\n    }\n}\n",
+                 "            atomicMin(qthr + myq[g], (unsigned long long)__double_as_longlong((double)thr[g]));\n    }\n    }\n    KB8S(3);\n}\n")):
+            assert s.count(old) == 1, old
+            s = s.replace(old, new)
+        return s
     if name == "count":
         s = COUNT_HDR + s
         for old, new in (

@@ -23,6 +23,14 @@ extern "C" int kb8_counts(unsigned long long *h)
 }
 #endif
 
+#ifdef KB8_STAMP
+// the stamp ablation's per-workgroup clocks: 4 words a workgroup
+extern "C" int kb8_stamps(unsigned long long *h, int nwg)
+{
+    return hipMemcpyFromSymbol(h, HIP_SYMBOL(kb8_stamp), sizeof(unsigned long long) * 4 * nwg) == hipSuccess ? 0 : -1;
+}
+#endif
+
 __global__ void kb8_fill_inf(double *p, int n)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;

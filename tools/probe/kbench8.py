@@ -99,6 +99,23 @@ def main():
         rec = {"workload": a.workload, "m": m, "nq": nq, "keep_qthr": a.keep_qthr, "ideal": a.ideal_qthr,
                "variant": var, "splits": splits, "ms": ms,
                "tops": flop / (ms * 1e-3) / 1e12 if ms > 0 else None}
+        stamps = getattr(L, "kb8_stamps", None)   # the "stamp" ablation only
+        if stamps is not None:
+            nwg = min(((nq + 127) // 128) * splits, 16384)
+            buf = (ctypes.c_ulonglong * (4 * nwg))()
+            stamps.argtypes = [p, i]
+            stamps(buf, nwg)
+            st = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 4).astype(np.int64)
+            t0 = st[:, 0].min()
+            us = lambda v: v * 0.01   # 100 MHz ticks
+            q = lambda v: [round(float(np.percentile(v, x)), 1) for x in (0, 10, 50, 90, 100)]
+            rec["stamps_us"] = {
+                "start_after_launch_p0_10_50_90_100": q(us(st[:, 0] - t0)),
+                "prologue": q(us(st[:, 1] - st[:, 0])),
+                "loop": q(us(st[:, 2] - st[:, 1])),
+                "end": q(us(st[:, 3] - st[:, 2])),
+                "wg_total": q(us(st[:, 3] - st[:, 0])),
+                "launch_span": round(float(us(st[:, 3].max() - t0)), 1)}
         if counts is not None:
             counts(cbuf)
             names = ("past_acc_filter", "keys_built", "exact_survivors", "extract_rounds", "merges")
