@@ -107,8 +107,7 @@ struct knn_ctx {
      * a direct-exchange pass alternates two launch sizes, and one model
      * evaluation costs ~0.5 ms of host time at 15000 queries */
 #define KNN_SPLIT_CACHE 8
-    struct { size_t nc; int lpq, i8, solo, klx, best, small; } split_cache[KNN_SPLIT_CACHE];
-    int split_small;    /* the last choose_splits: tiles of a short last split (knn_i8_blocks_t.small) */
+    struct { size_t nc; int lpq, i8, solo, klx, best; } split_cache[KNN_SPLIT_CACHE];
     int split_next;
     int nfail;
     int mode;
@@ -811,7 +810,6 @@ static double launch_makespan(long nqb, long ntiles, int s, int cus, double wgc)
  * own-block step, lane-list length): each of these changes s_min. */
 static int choose_splits(knn_ctx_t *c, size_t nc)
 {
-    c->split_small = 0;
     const char *env = getenv("KNN_SPLITS");
     /* (workgroups of 128 qg queries: knn_i8_qg) */
     const long qpw = (long)KNN_TQ * (c->i8 ? knn_i8_qg(c->klx, c->lpq, c->n) : 1);
@@ -833,10 +831,8 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     for (int e = 0; e < KNN_SPLIT_CACHE; e++)
         if (c->split_cache[e].best > 0 && c->split_cache[e].nc == nc && c->split_cache[e].lpq == c->lpq &&
             c->split_cache[e].i8 == c->i8 && c->split_cache[e].solo == c->split_solo &&
-            c->split_cache[e].klx == c->klx) {
-            c->split_small = c->split_cache[e].small;
+            c->split_cache[e].klx == c->klx)
             return c->split_cache[e].best;
-        }
     int smax = KNN_MAX_LISTS / c->lpq;
     const size_t per = split_bytes(c);
     if (per > 0 && KNN_PART_BUDGET / per < (size_t)smax)
@@ -896,27 +892,7 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         if (nqb * s_min < 2L * slots && s1 >= 1 && s1 < s_min &&
             (double)nc / ((double)s1 * c->lpq) <= 6000.0)
             best = (int)s1;
-        /* i8_tail: a grid of several rounds whose last round is at most half
-         * full (MNIST P = 1: 469 query blocks x 7 splits = 6.41 rounds of
-         * 512) idles most slots for a whole workgroup time at its end.  One
-         * more split, dispatched last (split-major order) and half as long
-         * as the others, fills that round instead: the s_min splits shrink
-         * to ntiles / (s_min + 1/2) tiles each (shorter lane lists than at
-         * s_min) and the tail to one half-length round.  (KNN_I8_TAIL=0:
-         * even splits.) */
-        int small = 0;
-        if (best == s_min && s_min + 1 <= smax && !(getenv("KNN_I8_TAIL") && getenv("KNN_I8_TAIL")[0] == '0')) {
-            const double r = (double)(nqb * s_min) / (double)slots;
-            const double fr = r - (double)(long)r;
-            const long sm = ntiles / (2L * s_min + 1);
-            if (fr > 0.0 && fr <= 0.5 && sm >= 1 && ntiles - sm >= s_min) {
-                best = s_min + 1;
-                small = (int)sm;
-            }
-        }
-        c->split_small = small;
         const int e = c->split_next++ % KNN_SPLIT_CACHE;
-        c->split_cache[e].small = small;
         c->split_cache[e].nc = nc;
         c->split_cache[e].lpq = c->lpq;
         c->split_cache[e].i8 = c->i8;
@@ -934,7 +910,6 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         }
     }
     const int e = c->split_next++ % KNN_SPLIT_CACHE;
-    c->split_cache[e].small = 0;
     c->split_cache[e].nc = nc;
     c->split_cache[e].lpq = c->lpq;
     c->split_cache[e].i8 = c->i8;
@@ -1165,7 +1140,6 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     RCHK(flush_pend2(c, NULL, NULL));   /* a deferred merge goes first, in step order */
     c->split_solo = c->i8 && c->nstep == 0 && !xb && d_sblock != NULL && d_sblock == c->q8 && nc == c->nq;
     int nsplit = choose_splits(c, nc);
-    const int nsplit_chosen = nsplit, split_small = c->split_small;
     {
         /* (diagnostic: the split count of a split-filter search's own-block
          * step, whose merge the fused step shares) */
@@ -1281,7 +1255,6 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
             tab.base[0] = (int64_t)c_base;
             tab.nc[0] = (int)nc;
         }
-        tab.small = nsplit == nsplit_chosen ? split_small : 0;
         RCHK(knn_launch_dist_i8(c->kp, c->klx, c->lpq, c->k, c->q8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
                                 knn_rows_pad(c->block_cap), (int)c->n, nsplit, c->part_d[set],
                                 c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr,

@@ -311,13 +311,9 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // the host counts 128-row tiles; this kernel's tiles hold TR rows
     constexpr int TS = 4 / TM;
     ntiles *= TS;
-    // split-major order dispatches the last split last: a short last split
-    // (cb.small) fills the grid's final, partial round of workgroups
-    const int sm = (cb.small > 0 && nsplit > 1) ? cb.small * TS : 0;
-    const int nbig = nsplit - (sm > 0 ? 1 : 0), tbig = ntiles - sm;
-    const int tb = tbig / nbig, tr = tbig - tb * nbig;
-    const int t_lo = split < nbig ? split * tb + (split < tr ? split : tr) : tbig;
-    const int t_hi = split < nbig ? t_lo + tb + (split < tr ? 1 : 0) : ntiles;
+    const int tb = ntiles / nsplit, tr = ntiles - tb * nsplit;
+    const int t_lo = split * tb + (split < tr ? split : tr);
+    const int t_hi = t_lo + tb + (split < tr ? 1 : 0);
     const int qrow0 = qb * QB;
     // query of group g; padding queries (>= nq) load row nq - 1 (with QG = 2
     // the last block may reach past the query block's rows) and reject all
@@ -1025,7 +1021,6 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int lpq, int k, const void *qs
     }
     const int ntiles = cb.t0[cb.nblk];
     if (nqb <= 0 || nsplit <= 0 || k <= 0 || k > kp || kl <= 0 || nks > 28) return KNN_ERR_INVALID;
-    if (cb.small < 0 || (cb.small > 0 && (nsplit < 2 || ntiles - cb.small < nsplit - 1))) return KNN_ERR_INVALID;
     // (QG = 2: the last block's padding queries load row nq - 1 and write nothing)
     if (qg == 1 && ((size_t)nqb * 128 > q_rows_pad || nq_pad < nqb * 128)) return KNN_ERR_INVALID;
     if ((size_t)nq > q_rows_pad || nq > nq_pad) return KNN_ERR_INVALID;

@@ -108,10 +108,6 @@ typedef struct {
     int nc[KNN_I8_MAXBLK];
     int t0[KNN_I8_MAXBLK + 1];
     int nblk;
-    /* > 0: the launch's last split takes `small` 128-row tiles and the
-     * others share the rest evenly (a short last split for grids of several
-     * rounds, knn_engine.c: i8_tail); 0: every split alike */
-    int small;
 } knn_i8_blocks_t;
 static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL_S : KNN_I8_KL_L; }
 /* lists per query: 2 for the 65-entry lists (k > 32) and for the 12-entry
