@@ -321,7 +321,7 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
             # -- a mismatch (new data) runs the search again, on every rank
             # alike: the reduced meta and the hint are the same everywhere
             h_meta = ring_hint
-            verify = engine.meta_host(engine.meta)
+            verify = True   # (read back behind the pass's steps, below)
         else:
             h_meta = engine.meta.cpu().numpy()   # the ring needs it on the host anyway
     spec = getattr(engine, "spec", False)
@@ -334,7 +334,7 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
             # behind the search and checked after it -- on a mismatch the
             # search runs again from the element block
             h_meta = hint
-            verify = engine.meta_host(engine.meta)
+            verify = True   # (read back behind the pass's steps, below)
         else:
             h_meta = engine.meta.cpu().numpy()   # (P = 1: begin would read it back anyway)
     if h_meta is not None and h_meta[7] != 0.0 and not engine.mk.s8_spec_ok(h_meta, engine.n, engine.dtype):
@@ -484,6 +484,11 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
         held = direct_pass(False, None)
     else:
         one_pass(0, False)
+    if verify is True:
+        # the meta's read-back, enqueued behind the steps: on the caller's
+        # stream it would sit between the pack and the search's first kernel
+        # (a 6 us copy on the critical path); end() waits for it
+        verify = engine.meta_host(engine.meta)
     unresolved = engine.end()
     if (unresolved > 0 and held_s and P > 1 and hasattr(engine, "research") and engine.ctx.shadow() == 2):
         # a ring rank's uncertified queries: searched again on the int8
@@ -492,8 +497,8 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
         unresolved = engine.research([x for x, _, _ in held_s], [r for _, _, r in held_s],
                                      [b for _, b, _ in held_s])
     if verify is not None and P == 1:
-        # (the read-back was enqueued before the search's first kernel, which
-        # the merge end() synchronised with waits for: it has landed)
+        # (the read-back was enqueued on the caller's stream before end(),
+        # which waits for that stream: it has landed)
         if not engine.mk.s8_spec_ok(verify.numpy(), engine.n, engine.dtype):
             engine.spec_hint = None   # not this data: the checked path, from the start
             return ring_search(dist, torch, engine, rank, P, m, q_base, schedule, timeout_s)
