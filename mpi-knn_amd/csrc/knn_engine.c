@@ -79,7 +79,7 @@ struct knn_ctx {
     /* overlapped step schedule (knn_ctx_step): distance kernels alternate
      * over two streams, merges run in order on a third */
     hipStream_t ds[2], ms;
-    hipEvent_t ev_in, ev_d[2], ev_m[KNN_PSETS], ev_ds[KNN_PSETS], ev_end;
+    hipEvent_t ev_in, ev_m[KNN_PSETS], ev_ds[KNN_PSETS], ev_end;
     int nstep;
     /* per-query filter bound shared by all splits and ring steps */
     double *qthr;
@@ -307,7 +307,6 @@ static void ctx_free_buffers(knn_ctx_t *c)
     }
     for (int b = 0; b < 2; b++) {
         if (c->ds[b]) hipStreamDestroy(c->ds[b]);
-        if (c->ev_d[b]) hipEventDestroy(c->ev_d[b]);
     }
     if (c->ms) hipStreamDestroy(c->ms);
     hipFree(c->qsh);
@@ -453,7 +452,6 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     ok &= c->h_count && hipHostGetDevicePointer((void **)&c->h_count_dev, c->h_count, 0) == hipSuccess;
     for (int b = 0; b < 2; b++) {
         ok &= hipStreamCreateWithFlags(&c->ds[b], hipStreamNonBlocking) == hipSuccess;
-        ok &= hipEventCreateWithFlags(&c->ev_d[b], hipEventDisableTiming) == hipSuccess;
     }
     for (int b = 0; b < KNN_PSETS; b++) {
         ok &= hipEventCreateWithFlags(&c->ev_m[b], hipEventDisableTiming) == hipSuccess;
@@ -1084,8 +1082,8 @@ static int merge_pending(knn_ctx_t *c) { return merge_pending_fin(c, NULL, NULL)
  * set p = s % 4 and k_merge on stream ms (high priority), in step order:
  *   ds[s%2]: wait ev_in (the caller's stream at this call: the block has
  *            arrived, begin() is done) and ev_m[p] (merge s-4 has read the
- *            partial set), then k_dist_topk(s)              -> ev_d[s%2]
- *   ms:      wait ev_d[s%2] (implies ev_in), then k_merge(s) -> ev_m[p]
+ *            partial set), then k_dist_topk(s)              -> ev_ds[p]
+ *   ms:      wait ev_ds[p] (implies ev_in), then k_merge(s) -> ev_m[p]
  *   caller:  wait ev_m[(s-2)%4] (step s-2 has finished reading its block);
  *            exact-integer contractions (int8 / fp16: k_merge never reads
  *            block rows) wait ev_ds[(s-2)%4], k_dist_topk(s-2) alone, so
@@ -1269,15 +1267,16 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
                                       (c->split && env_on("KNN_SPLIT_V1") ? KNN_DIST_SPLIT_V1 : 0),
                                   c->split ? (float)(-2.0 / ((double)c->sscale * c->sscale)) : -2.f, ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
-    HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
-    HIPCHK(hipEventRecord(c->ev_ds[set], ds));
-    /* (the distance kernel waited for ev_in: ev_d covers the block's
+    /* one event a step behind its distance kernel (each record is a marker
+     * packet on the queue, ~5 us before whatever follows it there): the
+     * merge stream, the caller's lag wait and knn_ctx_end all use ev_ds.
+     * (The distance kernel waited for ev_in: ev_ds covers the block's
      * arrival too -- a second wait would add its own latency) */
-    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));
+    HIPCHK(hipEventRecord(c->ev_ds[set], ds));
+    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_ds[set], 0));
     if (pairing) {
-        /* the pending even step's kernel signalled ev_d[ds_i ^ 1], not yet
-         * re-recorded (the next record is step s+1's) */
-        HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i ^ 1], 0));
+        /* the pending even step (step s - 1, on the other distance stream) */
+        HIPCHK(hipStreamWaitEvent(c->ms, c->ev_ds[(set + KNN_PSETS - 1) % KNN_PSETS], 0));
         c->pend = 0;
         if (xb && rank_merge_ok(c, c->pend_nsplit + nsplit)) {
             /* the fused step (the direct exchange's last): its merge waits
@@ -1436,14 +1435,13 @@ static int ctx_step_split_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks
                                  (int)c->nq_pad, c->qthr, c->xord, (float)(-2.0 / ((double)c->sscale * c->sscale)),
                                  ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
-    HIPCHK(hipEventRecord(c->ev_d[ds_i], ds));
     HIPCHK(hipEventRecord(c->ev_ds[set], ds));
-    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i], 0));
+    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_ds[set], 0));
     int mset = set, mnsplit = nsplit;
     hipEvent_t *pev = NULL;
     if (share) {
         /* one merge of both steps: the pending set's lists, then this one's */
-        HIPCHK(hipStreamWaitEvent(c->ms, c->ev_d[ds_i ^ 1], 0));
+        HIPCHK(hipStreamWaitEvent(c->ms, c->ev_ds[(set + KNN_PSETS - 1) % KNN_PSETS], 0));
         c->pend = 0;
         mb.ptr[nblk] = c->pend_cblk;
         mb.base[nblk] = (int64_t)c->pend_cbase;
@@ -1725,7 +1723,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     hipStream_t ms = c->ms;
     if (!c->merged && c->nstep >= 1 && !env_on("KNN_END_ON_MS")) {
         const int last = (c->nstep - 1) & 1;
-        if (c->nstep >= 2) HIPCHK(hipEventSynchronize(c->ev_d[last ^ 1]));
+        if (c->nstep >= 2) HIPCHK(hipEventSynchronize(c->ev_ds[(c->nstep - 2) % KNN_PSETS]));
         c->ms = c->ds[last];
     }
     const int rc_end = ctx_end_merge(c, d_out, s);
