@@ -1688,9 +1688,10 @@ static int ctx_end_merge(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
                                  c->split, c->ms));
     c->h_count[0] = c->h_count[1] = -1;
     RCHK(knn_launch_count_out(c->fail_count, c->h_count_dev, c->ms));
-    HIPCHK(hipEventRecord(c->ev_end, c->ms));
-    HIPCHK(hipStreamWaitEvent(s, c->ev_end, 0));
+    /* the host waits for the results, so the caller's stream needs no wait
+     * packet on them (one would sit before that stream's next kernel) */
     HIPCHK(hipStreamSynchronize(c->ms));
+    (void)s;
     return KNN_OK;
 }
 
@@ -1709,7 +1710,8 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
      * that stream first waits for the caller's stream as it stands now:
      * d_out may have just been allocated, cleared or read there (a caching
      * allocator hands out memory that pending work on the caller's stream
-     * used last).  The caller's stream is ordered after the results. */
+     * used last).  end() returns with the results complete (a host wait), so
+     * whatever the caller enqueues afterwards follows them. */
     /* The orderings end() needs besides the last distance launch -- the
      * caller's stream as it stands now, and the other distance stream's last
      * launch -- are waited for on the HOST: end() blocks until the results
