@@ -1672,9 +1672,9 @@ static int ctx_end_device(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
     return KNN_OK;
 }
 
-/* knn_ctx_end's device part and count read-back, on stream c->ms; the
- * caller's stream has been waited for on the host (end_wait) */
-static int ctx_end_merge(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
+/* knn_ctx_end's device part and count read-back, on stream c->ms (the
+ * caller's stream has been waited for on the host) */
+static int ctx_end_merge(knn_ctx_t *c, knn_neighbour_t *d_out)
 {
     /* the last merge (deferred or pending) finalizes too when it is the
      * rank merge (INT-mode int8 lists) */
@@ -1691,7 +1691,6 @@ static int ctx_end_merge(knn_ctx_t *c, knn_neighbour_t *d_out, hipStream_t s)
     /* the host waits for the results, so the caller's stream needs no wait
      * packet on them (one would sit before that stream's next kernel) */
     HIPCHK(hipStreamSynchronize(c->ms));
-    (void)s;
     return KNN_OK;
 }
 
@@ -1728,7 +1727,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
         if (c->nstep >= 2) HIPCHK(hipEventSynchronize(c->ev_ds[(c->nstep - 2) % KNN_PSETS]));
         c->ms = c->ds[last];
     }
-    const int rc_end = ctx_end_merge(c, d_out, s);
+    const int rc_end = ctx_end_merge(c, d_out);
     c->ms = ms;
     RCHK(rc_end);
     RCHK(prof_collect(c));
