@@ -294,24 +294,29 @@ __device__ __forceinline__ int knn_spec8(T v)
     return (int)c - 128;
 }
 
-// col-major source (the .mat layout): a workgroup owns 64 rows and walks the
-// columns in 64 x 64 tiles (each wave reads 64 consecutive rows of a column:
-// 512-byte runs), all 16 loads of a thread's tile in flight before their
+// col-major source (the .mat layout): a workgroup owns RW rows and walks
+// the columns in 64-column tiles (RW = 64: each wave reads 64 consecutive
+// rows of one column, 512-byte runs; RW = 32: two columns of 32 rows a
+// wave), all of a thread's loads of a tile in flight before their
 // conversion; bytes go through LDS into 16-byte row stores.  Thread (ty, tx)
-// sums row tx's squares over columns = ty mod 4; four partials a row.
-// (Issuing the next tile's 16 loads before converting this one -- 32 in
-// flight -- measured slower: 106 -> 130 us for MNIST, rocprofv3.)
-template <typename T, typename S>
+// sums row tx's squares over columns = ty mod (256 / RW); the partials add
+// exactly for the integer data the byte block holds (the meta decides
+// that; rejected data is packed again from elements).
+// (Issuing the next tile's loads before converting this one -- 32 in
+// flight at RW = 64 -- measured slower: 106 -> 130 us for MNIST, rocprofv3.)
+template <typename T, typename S, int RW>
 __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst, size_t rows, size_t rows_pad,
                                                    int n, int rs, const S *__restrict__ src, size_t ld)
 {
-    __shared__ unsigned char tb[64][68];   // [column of the tile][row]
-    __shared__ double part[4][64];
-    __shared__ unsigned ipart[4][64];
+    constexpr int CG = 256 / RW;      // column groups
+    constexpr int NE = 64 / CG;       // loads a thread a tile
+    __shared__ unsigned char tb[64][RW + 4];   // [column of the tile][row]
+    __shared__ double part[CG][RW];
+    __shared__ unsigned ipart[CG][RW];
     int *norms = (int *)(dst + rows_pad * (size_t)rs);
     double *meta = (double *)(norms + 2 * rows_pad);
-    const size_t i0 = (size_t)blockIdx.x * 64;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const size_t i0 = (size_t)blockIdx.x * RW;
+    const int tx = threadIdx.x % RW, ty = threadIdx.x / RW;
     const size_t i = i0 + tx;
     const bool live = i < rows;
     const S *xp = src + (live ? i : 0);
@@ -319,24 +324,24 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
     double s = 0.0;
     unsigned si = 0u;
     for (int j0 = 0; j0 < rs; j0 += 64) {
-        S v[16];
+        S v[NE];
 #pragma unroll
-        for (int e = 0; e < 16; e++) {
-            const int j = j0 + ty + 4 * e;
+        for (int e = 0; e < NE; e++) {
+            const int j = j0 + ty + CG * e;
             v[e] = (live && j < n) ? __builtin_nontemporal_load(xp + (size_t)j * ld) : (S)0;
         }
 #pragma unroll
-        for (int e = 0; e < 16; e++) {
+        for (int e = 0; e < NE; e++) {
             const T x = (T)v[e];
             ma.add((double)x, s);
-            const int xi = (live && j0 + ty + 4 * e < n) ? knn_spec8(x) : 0;
+            const int xi = (live && j0 + ty + CG * e < n) ? knn_spec8(x) : 0;
             si += (unsigned)(xi * xi);
-            tb[ty + 4 * e][tx] = (unsigned char)xi;
+            tb[ty + CG * e][tx] = (unsigned char)xi;
         }
         __syncthreads();
         // row r = t / 4: 16 bytes at column 16 (t % 4) of the tile
         const int r = threadIdx.x >> 2, c0 = 16 * (threadIdx.x & 3);
-        if (i0 + r < rows_pad && j0 + c0 < rs) {
+        if (r < RW && i0 + r < rows_pad && j0 + c0 < rs) {
             unsigned w4[4];
 #pragma unroll
             for (int q = 0; q < 4; q++)
@@ -351,8 +356,18 @@ __global__ __launch_bounds__(256) void k_pack8_col(signed char *__restrict__ dst
     __syncthreads();
     double mnorm = 0.0;
     if (ty == 0 && i < rows_pad) {
-        const double nr = (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]);
-        const unsigned ni = (ipart[0][tx] + ipart[1][tx]) + (ipart[2][tx] + ipart[3][tx]);
+        double nr = 0.0;
+        unsigned ni = 0u;
+        if constexpr (CG == 4) {
+            nr = (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]);
+            ni = (ipart[0][tx] + ipart[1][tx]) + (ipart[2][tx] + ipart[3][tx]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < CG; q++) {
+                nr += part[q][tx];
+                ni += ipart[q][tx];
+            }
+        }
         norms[i8_norm_pos((int)i)] = i8_norm_word((int)i, (int)ni, rs);
         norms[rows_pad + i8_norm_pos((int)i)] = i8_init_word((int)ni, rs);
         if (nr == nr) mnorm = nr;
@@ -2126,8 +2141,13 @@ static int launch_pack8(signed char *dst, size_t cap, size_t rows, size_t n, con
     double *meta = (double *)(dst + knn_s8_meta_offset(cap, n));
     if (hipMemsetAsync(meta, 0, KNN_META_DOUBLES * sizeof(double), s) != hipSuccess) return KNN_ERR_HIP;
     if (layout == KNN_COLMAJOR) {
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_col<T, S>), dim3((unsigned)((rp + 63) / 64)), dim3(256), 0, s,
-                           dst, rows, rp, (int)n, (int)rs, src, ld);
+        const char *e32 = getenv("KNN_PACK8_RW");
+        if (e32 && atoi(e32) == 32)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_col<T, S, 32>), dim3((unsigned)((rp + 31) / 32)), dim3(256), 0,
+                               s, dst, rows, rp, (int)n, (int)rs, src, ld);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_col<T, S, 64>), dim3((unsigned)((rp + 63) / 64)), dim3(256), 0,
+                               s, dst, rows, rp, (int)n, (int)rs, src, ld);
     } else {
         const unsigned nb = (unsigned)((rp + 3) / 4 < 8192 ? (rp + 3) / 4 : 8192);
         const bool vec = ((uintptr_t)src % 16 == 0) && (ld * sizeof(S)) % 16 == 0;
