@@ -2141,13 +2141,9 @@ static int launch_pack8(signed char *dst, size_t cap, size_t rows, size_t n, con
     double *meta = (double *)(dst + knn_s8_meta_offset(cap, n));
     if (hipMemsetAsync(meta, 0, KNN_META_DOUBLES * sizeof(double), s) != hipSuccess) return KNN_ERR_HIP;
     if (layout == KNN_COLMAJOR) {
-        const char *e32 = getenv("KNN_PACK8_RW");
-        if (e32 && atoi(e32) == 32)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_col<T, S, 32>), dim3((unsigned)((rp + 31) / 32)), dim3(256), 0,
-                               s, dst, rows, rp, (int)n, (int)rs, src, ld);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_col<T, S, 64>), dim3((unsigned)((rp + 63) / 64)), dim3(256), 0,
-                               s, dst, rows, rp, (int)n, (int)rs, src, ld);
+        // (32-row workgroups, twice as many: 107.5 against 105.7 us for MNIST)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_pack8_col<T, S, 64>), dim3((unsigned)((rp + 63) / 64)), dim3(256), 0,
+                           s, dst, rows, rp, (int)n, (int)rs, src, ld);
     } else {
         const unsigned nb = (unsigned)((rp + 3) / 4 < 8192 ? (rp + 3) / 4 : 8192);
         const bool vec = ((uintptr_t)src % 16 == 0) && (ld * sizeof(S)) % 16 == 0;
