@@ -68,6 +68,9 @@ typedef _Float16 knn_sh8 __attribute__((ext_vector_type(8)));
 #ifndef SP_ABL_NODMA
 #define SP_ABL_NODMA 0
 #endif
+#ifndef SP_D_SMALL   /* A-fragment prefetch depth (m-tiles) of the <= 24-entry kernels */
+#define SP_D_SMALL 4
+#endif
 #ifndef SP_NOPRE   /* (diagnostic: no next-chunk fragment prefetch) */
 #define SP_NOPRE 0
 #endif
@@ -823,7 +826,7 @@ extern "C" int knn_launch_dist_split(int dtype, int kl, const void *qsp, const v
     if (cb.t0[cb.nblk] < nsplit) return KNN_ERR_INVALID;
     hipStream_t s = (hipStream_t)stream;
 #define SPL(T, KL)                                                                                          \
-    return launch_split<T, KL, (KL > 24 ? 2 : 4)>(qsp, (const T *)qnorm, q_base, nq, cb, n, meta, nsplit, part_d, \
+    return launch_split<T, KL, (KL > 24 ? 2 : SP_D_SMALL)>(qsp, (const T *)qnorm, q_base, nq, cb, n, meta, nsplit, part_d, \
                                                  part_i, part_T, nq_pad, qthr, uj, xord, m2s, s)
     if (dtype == KNN_F64 && kl == KNN_KL) SPL(double, KNN_KL);
     if (dtype == KNN_F32 && kl == KNN_KL) SPL(float, KNN_KL);
