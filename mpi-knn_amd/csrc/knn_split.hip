@@ -71,6 +71,11 @@ typedef _Float16 knn_sh8 __attribute__((ext_vector_type(8)));
 #ifndef SP_D_SMALL   /* A-fragment prefetch depth (m-tiles) of the <= 24-entry kernels */
 #define SP_D_SMALL 4
 #endif
+// (D must divide the 16 m-tiles: the next chunk's first D fragments are read
+// into the slots mt % D of the current chunk's last D m-tiles, and the next
+// chunk reads m-tile j from slot j % D -- a D = 3 build failed the parity
+// tests, tools/r05_s37.sh)
+
 #ifndef SP_NOPRE   /* (diagnostic: no next-chunk fragment prefetch) */
 #define SP_NOPRE 0
 #endif
@@ -96,6 +101,7 @@ __global__ __launch_bounds__(512) void k_dist_split(
     unsigned long long *__restrict__ qthr, int uj, int xord, float m2s)
 {
     constexpr int ES = (int)sizeof(T);
+    static_assert(16 % D == 0, "fragment depth must divide the 16 m-tiles (next-chunk prefetch slots)");
     __shared__ __attribute__((aligned(16))) char smem[SP_LDS];
     LDS_AS char *lds = (LDS_AS char *)smem;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
