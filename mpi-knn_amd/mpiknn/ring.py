@@ -510,7 +510,12 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
         engine.ring_hint = np.array(h_meta, dtype=np.float64, copy=True)
     total = unresolved
     if P > 1:
-        t = torch.tensor([float(unresolved)], dtype=torch.float64, device=engine.meta.device)
+        # (a buffer kept on the engine: filled in place, no host-to-device
+        # copy a pass)
+        t = getattr(engine, "_unres_buf", None)
+        if t is None or t.device != engine.meta.device:
+            t = engine._unres_buf = torch.zeros(1, dtype=torch.float64, device=engine.meta.device)
+        t.fill_(float(unresolved))
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         total = int(t.item())
     if total > 0 and spec:
