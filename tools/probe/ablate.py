@@ -13,6 +13,12 @@ with  KB8_SO=tools/probe/abl/libkbench8_<name>.so python tools/probe/kbench8.py
   noepi_nowait   pieces issued, never waited for (racy: timing only)
   stamp        the product kernel plus per-workgroup wall-clock stamps
                (s_memrealtime at start, first chunk ready, loop done, end)
+  tri          each query block scans only the tiles from its own rows on
+               (the upper triangle of the self-join; its splits share that
+               range): half the MFMA work (timing only, results partial)
+  tricol       tri plus a column-direction filter in the epilogue (per-row
+               thresholds from LDS against 2 acc - |q'|^2, ballot, no
+               emission): the estimate of a symmetric kernel (timing only)
   count        the product kernel plus per-wave event counters (one vector
                atomic a wave and event, lane 0): groups past the init-word
                filter (all groups where it is off), groups whose exact keys
@@ -81,6 +87,37 @@ def patch(s, name):
             assert old in s, old
             s = s.replace(old, new)
         return s
+    if name.startswith("tri"):
+        old = ("    const int tb = ntiles / nsplit, tr = ntiles - tb * nsplit;\n"
+               "    const int t_lo = split * tb + (split < tr ? split : tr);\n"
+               "    const int t_hi = t_lo + tb + (split < tr ? 1 : 0);\n")
+        assert s.count(old) == 1
+        s = s.replace(old, "    const int tq0_ = (qb * QB) / TR, nt2_ = ntiles - tq0_;\n"
+                           "    const int tb = nt2_ / nsplit, tr = nt2_ - tb * nsplit;\n"
+                           "    const int t_lo = tq0_ + split * tb + (split < tr ? split : tr);\n"
+                           "    const int t_hi = t_lo + tb + (split < tr ? 1 : 0);\n")
+    if name == "tricol":
+        old = "            int T = thr_v(g);\n            int vm = i8_max32(v);\n"
+        assert s.count(old) == 1
+        s = s.replace(old, """            {   // column direction: row r's threshold |r'|^2 - lim_r (init-word slots)
+                int cm = 0;
+#pragma unroll
+                for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const knn_v4i t4 = *(const LDS_AS knn_v4i *)(cn + NSEG / 2 + nofs(4 * h + 8 * (MB * rh + 2 * pr + bb) + j));
+#pragma unroll
+                        for (int i = 0; i < 4; i++) cm |= (2 * a[16 * bb + 4 * j + i] - qn[g] >= t4[i]) ? 1 : 0;
+                    }
+                colsink ^= (unsigned)__ballot(cm);
+            }
+""" + old)
+        old = "    long c_base = 0;\n"
+        assert s.count(old) == 1
+        s = s.replace(old, "    unsigned colsink = 0;\n" + old)
+        old = "#pragma unroll\n    for (int g = 0; g < QG; g++) merge(g);\n"
+        assert s.count(old) == 1
+        s = s.replace(old, old + "    if (colsink == 0x9e3779b9u) part_T[0] = 2.0;\n")
     if "noepi" in name:
         old = "            epilogue(t, acc, x);\n"
         assert old in s
