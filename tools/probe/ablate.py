@@ -19,6 +19,13 @@ with  KB8_SO=tools/probe/abl/libkbench8_<name>.so python tools/probe/kbench8.py
   tricol       tri plus a column-direction filter in the epilogue (per-row
                thresholds from LDS against 2 acc - |q'|^2, ballot, no
                emission): the estimate of a symmetric kernel (timing only)
+  sym          the self-join's symmetric launch (tools/probe/ksym.hip): an
+               extra argument block; sy_mode 1 restricts each query block to
+               the tiles from its own rows on (the first sy_qa blocks: from
+               row 128 sy_qa on, row direction only) and adds the column
+               direction on the tiles past the block's own: per-row
+               thresholds w = lim - |r'|^2 staged as the (unused, long-row)
+               init words, survivors appended to a per-workgroup region
   count        the product kernel plus per-wave event counters (one vector
                atomic a wave and event, lane 0): groups past the init-word
                filter (all groups where it is off), groups whose exact keys
@@ -118,6 +125,81 @@ def patch(s, name):
         old = "#pragma unroll\n    for (int g = 0; g < QG; g++) merge(g);\n"
         assert s.count(old) == 1
         s = s.replace(old, old + "    if (colsink == 0x9e3779b9u) part_T[0] = 2.0;\n")
+    if name == "sym":
+        for old, new in (
+                ("    unsigned long long *__restrict__ qthr, int uj, unsigned long long *__restrict__ qsum)\n{\n",
+                 "    unsigned long long *__restrict__ qthr, int uj, unsigned long long *__restrict__ qsum,\n"
+                 "    int sy_mode, int sy_qa, unsigned *__restrict__ sy_wcnt, uint4 *__restrict__ sy_buf, int sy_wcap)\n{\n"),
+                ("                       KL != KNN_I8_KL_L ? qsum : nullptr);\n",
+                 "                       KL != KNN_I8_KL_L ? qsum : nullptr, 0, 0, nullptr, nullptr, 0);\n"),
+                ("    __shared__ __attribute__((aligned(16))) char smem[LDSB];\n",
+                 "    __shared__ __attribute__((aligned(16))) char smem[LDSB];\n    __shared__ unsigned sy_n;\n"),
+                ("    const int tb = ntiles / nsplit, tr = ntiles - tb * nsplit;\n"
+                 "    const int t_lo = split * tb + (split < tr ? split : tr);\n"
+                 "    const int t_hi = t_lo + tb + (split < tr ? 1 : 0);\n",
+                 "    const int sy_t0 = sy_mode ? (qb < sy_qa ? sy_qa * 128 / TR : qb * QB / TR) : 0;\n"
+                 "    const int sy_ct0 = (sy_mode && qb >= sy_qa) ? (qb + 1) * QB / TR : 0x7fffffff;\n"
+                 "    const int sy_nt = ntiles - sy_t0;\n"
+                 "    const int tb = sy_nt / nsplit, tr = sy_nt - tb * nsplit;\n"
+                 "    const int t_lo = sy_t0 + split * tb + (split < tr ? split : tr);\n"
+                 "    const int t_hi = t_lo + tb + (split < tr ? 1 : 0);\n"),
+                ("    __syncthreads();\n\n    // ---- staging ----",
+                 "    if (threadIdx.x == 0) sy_n = 0;\n    __syncthreads();\n\n    // ---- staging ----"),
+                ("            // exact keys of the group (slot words from the norm ring)\n",
+                 """            if (t >= sy_ct0 && myq[g] < nq) {
+                // column direction: candidate = this lane's query for the
+                // tile's rows as queries; w = lim_r - |r'|^2 (init-word slots):
+                // d^2 <= lim_r <=> 2 acc + w >= |q'|^2
+                int cmax = (int)0x80000000;
+#pragma unroll
+                for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const knn_v4i w4 = *(const LDS_AS knn_v4i *)(cn + NSEG / 2 + nofs(4 * h + 8 * (MB * rh + 2 * pr + bb) + j));
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const int x = 16 * bb + 4 * j + i;
+                            int c = (int)((unsigned)a[x] * 2u + (unsigned)w4[i]);
+                            if (masked) c = a[x] == A_NONE ? (int)0x80000000 : c;
+                            cmax = c > cmax ? c : cmax;
+                        }
+                    }
+                if (__ballot(cmax >= qn[g]) != 0ull && cmax >= qn[g]) {
+#pragma unroll
+                    for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const knn_v4i w4 = *(const LDS_AS knn_v4i *)(cn + NSEG / 2 + nofs(4 * h + 8 * (MB * rh + 2 * pr + bb) + j));
+                            const knn_v4i k4 = *(const LDS_AS knn_v4i *)(cn + nofs(4 * h + 8 * (MB * rh + 2 * pr + bb) + j));
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int x = 16 * bb + 4 * j + i;
+                                const int c = (int)((unsigned)a[x] * 2u + (unsigned)w4[i]);
+                                if (c >= qn[g] && !(masked && a[x] == A_NONE)) {
+                                    const int d2 = qn[g] - (k4[i] >> 5) - 2 * a[x];
+                                    if (d2 > 0) {
+                                        const unsigned sl = atomicAdd(&sy_n, 1u);
+                                        if ((int)sl < sy_wcap)
+                                            sy_buf[(size_t)blockIdx.x * sy_wcap + sl] =
+                                                make_uint4((unsigned)(idb + 32 * (2 * pr + bb) + 8 * j + i), (unsigned)d2,
+                                                           (unsigned)gq[g], 0u);
+                                    }
+                                }
+                            }
+                        }
+                }
+            }
+            // exact keys of the group (slot words from the norm ring)
+"""),
+                ("            atomicMin(qthr + myq[g], (unsigned long long)__double_as_longlong((double)thr[g]));\n    }\n    }\n}\n",
+                 "            atomicMin(qthr + myq[g], (unsigned long long)__double_as_longlong((double)thr[g]));\n    }\n    }\n"
+                 "    if (sy_mode) {\n        __syncthreads();\n        if (threadIdx.x == 0) sy_wcnt[blockIdx.x] = sy_n;\n    }\n}\n"),
+                # (no cross-split summaries: their registers go to the column path)
+                ("    constexpr bool SUM = REREAD && KL == KNN_I8_KL_S && QG == 1;\n",
+                 "    constexpr bool SUM = false;\n")):
+            assert s.count(old) == 1, old[:70]
+            s = s.replace(old, new)
+        return s
     if "noepi" in name:
         old = "            epilogue(t, acc, x);\n"
         assert old in s
@@ -170,11 +252,12 @@ def main():
         f = os.path.join(out, "knn_i8_%s.hip" % name)
         open(f, "w").write(patch(src, name))
         so = os.path.join(out, "libkbench8_%s.so" % name)
+        harness = "ksym.hip" if name == "sym" else "kbench8.hip"
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-I" + os.path.join(HERE, "..", "..", "include"),
                "-I" + os.path.join(HERE, "..", "..", "mpi-knn_amd", "csrc"),
                "-mllvm", "-disable-promote-alloca-to-lds", '-DKB8_SRC="%s"' % f, "-o", so,
-               os.path.join(HERE, "kbench8.hip")]
+               os.path.join(HERE, harness)]
         subprocess.check_call(cmd)
         print(so)
 
