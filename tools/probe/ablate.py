@@ -196,7 +196,11 @@ def patch(s, name):
                  "    if (sy_mode) {\n        __syncthreads();\n        if (threadIdx.x == 0) sy_wcnt[blockIdx.x] = sy_n;\n    }\n}\n"),
                 # (no cross-split summaries: their registers go to the column path)
                 ("    constexpr bool SUM = REREAD && KL == KNN_I8_KL_S && QG == 1;\n",
-                 "    constexpr bool SUM = false;\n")):
+                 "    constexpr bool SUM = false;\n"),
+                # (long rows: the norm is the slot word's alone -- the init
+                # words carry the column thresholds here)
+                ("        qn[g] = i8_norm_of(qnorms[i8_norm_pos(lq[g])], qnorms[q_rows_pad + i8_norm_pos(lq[g])]);\n",
+                 "        qn[g] = -(qnorms[i8_norm_pos(lq[g])] >> 5);\n")):
             assert s.count(old) == 1, old[:70]
             s = s.replace(old, new)
         return s
