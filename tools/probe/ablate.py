@@ -125,7 +125,7 @@ def patch(s, name):
         old = "#pragma unroll\n    for (int g = 0; g < QG; g++) merge(g);\n"
         assert s.count(old) == 1
         s = s.replace(old, old + "    if (colsink == 0x9e3779b9u) part_T[0] = 2.0;\n")
-    if name == "sym":
+    if name.startswith("sym"):
         for old, new in (
                 ("    unsigned long long *__restrict__ qthr, int uj, unsigned long long *__restrict__ qsum)\n{\n",
                  "    unsigned long long *__restrict__ qthr, int uj, unsigned long long *__restrict__ qsum,\n"
@@ -146,16 +146,17 @@ def patch(s, name):
                 ("    __syncthreads();\n\n    // ---- staging ----",
                  "    if (threadIdx.x == 0) sy_n = 0;\n    __syncthreads();\n\n    // ---- staging ----"),
                 ("            // exact keys of the group (slot words from the norm ring)\n",
-                 """            if (t >= sy_ct0 && myq[g] < nq) {
+                 """            if (WPW / 4 == 4 && !SHORT && t >= sy_ct0 && myq[g] < nq) {   // (the 64-row long-row kernel)
                 // column direction: candidate = this lane's query for the
                 // tile's rows as queries; w = lim_r - |r'|^2 (init-word slots):
                 // d^2 <= lim_r <=> 2 acc + w >= |q'|^2
+                const LDS_AS char *cnh = cn + h * NSEG;   // nofs(4h + 8m + j) = (h + 2m) NSEG + 16 j
                 int cmax = (int)0x80000000;
 #pragma unroll
                 for (int bb = 0; bb < 2; bb++)
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        const knn_v4i w4 = *(const LDS_AS knn_v4i *)(cn + NSEG / 2 + nofs(4 * h + 8 * (MB * rh + 2 * pr + bb) + j));
+                        const knn_v4i w4 = *(const LDS_AS knn_v4i *)(cnh + (NSEG / 2 + 2 * (MB * rh + 2 * pr + bb) * NSEG + 16 * j));
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
                             const int x = 16 * bb + 4 * j + i;
@@ -169,8 +170,8 @@ def patch(s, name):
                     for (int bb = 0; bb < 2; bb++)
 #pragma unroll
                         for (int j = 0; j < 4; j++) {
-                            const knn_v4i w4 = *(const LDS_AS knn_v4i *)(cn + NSEG / 2 + nofs(4 * h + 8 * (MB * rh + 2 * pr + bb) + j));
-                            const knn_v4i k4 = *(const LDS_AS knn_v4i *)(cn + nofs(4 * h + 8 * (MB * rh + 2 * pr + bb) + j));
+                            const knn_v4i w4 = *(const LDS_AS knn_v4i *)(cnh + (NSEG / 2 + 2 * (MB * rh + 2 * pr + bb) * NSEG + 16 * j));
+                            const knn_v4i k4 = *(const LDS_AS knn_v4i *)(cnh + (2 * (MB * rh + 2 * pr + bb) * NSEG + 16 * j));
 #pragma unroll
                             for (int i = 0; i < 4; i++) {
                                 const int x = 16 * bb + 4 * j + i;
@@ -203,6 +204,10 @@ def patch(s, name):
                  "        qn[g] = -(qnorms[i8_norm_pos(lq[g])] >> 5);\n")):
             assert s.count(old) == 1, old[:70]
             s = s.replace(old, new)
+        if name == "sym_nostore":   # survivors counted, not stored (timing only)
+            old = "                                        if ((int)sl < sy_wcap)\n"
+            assert s.count(old) == 1
+            s = s.replace(old, "                                        if ((int)sl < 0)\n")
         return s
     if "noepi" in name:
         old = "            epilogue(t, acc, x);\n"
@@ -256,7 +261,7 @@ def main():
         f = os.path.join(out, "knn_i8_%s.hip" % name)
         open(f, "w").write(patch(src, name))
         so = os.path.join(out, "libkbench8_%s.so" % name)
-        harness = "ksym.hip" if name == "sym" else "kbench8.hip"
+        harness = "ksym.hip" if name.startswith("sym") else "kbench8.hip"
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-I" + os.path.join(HERE, "..", "..", "include"),
                "-I" + os.path.join(HERE, "..", "..", "mpi-knn_amd", "csrc"),
