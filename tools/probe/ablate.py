@@ -146,7 +146,7 @@ def patch(s, name):
                 ("    __syncthreads();\n\n    // ---- staging ----",
                  "    if (threadIdx.x == 0) sy_n = 0;\n    __syncthreads();\n\n    // ---- staging ----"),
                 ("            // exact keys of the group (slot words from the norm ring)\n",
-                 """            if (WPW / 4 == 4 && !SHORT && t >= sy_ct0 && myq[g] < nq) {   // (the 64-row long-row kernel)
+                 """            if (WPW / 4 == 4 && !SHORT && t >= sy_ct0) {   // (wave-uniform: the ballots below see every lane)   // (the 64-row long-row kernel)
                 // column direction: candidate = this lane's query for the
                 // tile's rows as queries; w = lim_r - |r'|^2 (init-word slots):
                 // d^2 <= lim_r <=> 2 acc + w >= |q'|^2
@@ -165,29 +165,59 @@ def patch(s, name):
                             cmax = c > cmax ? c : cmax;
                         }
                     }
-                if (__ballot(cmax >= qn[g]) != 0ull && cmax >= qn[g]) {
+                if (myq[g] >= nq) cmax = (int)0x80000000;   // padding queries are nobody's candidates
+                if (__ballot(cmax >= qn[g]) != 0ull) {
+                    // the lane's survivors as a mask, one LDS atomic a wave
+                    // (the wave's total), each lane's slots from a bit-sliced
+                    // prefix of the counts
+                    unsigned cm = 0;
 #pragma unroll
                     for (int bb = 0; bb < 2; bb++)
 #pragma unroll
                         for (int j = 0; j < 4; j++) {
                             const knn_v4i w4 = *(const LDS_AS knn_v4i *)(cnh + (NSEG / 2 + 2 * (MB * rh + 2 * pr + bb) * NSEG + 16 * j));
-                            const knn_v4i k4 = *(const LDS_AS knn_v4i *)(cnh + (2 * (MB * rh + 2 * pr + bb) * NSEG + 16 * j));
 #pragma unroll
                             for (int i = 0; i < 4; i++) {
                                 const int x = 16 * bb + 4 * j + i;
                                 const int c = (int)((unsigned)a[x] * 2u + (unsigned)w4[i]);
-                                if (c >= qn[g] && !(masked && a[x] == A_NONE)) {
-                                    const int d2 = qn[g] - (k4[i] >> 5) - 2 * a[x];
-                                    if (d2 > 0) {
-                                        const unsigned sl = atomicAdd(&sy_n, 1u);
-                                        if ((int)sl < sy_wcap)
-                                            sy_buf[(size_t)blockIdx.x * sy_wcap + sl] =
-                                                make_uint4((unsigned)(idb + 32 * (2 * pr + bb) + 8 * j + i), (unsigned)d2,
-                                                           (unsigned)gq[g], 0u);
+                                const bool ok = c >= qn[g] && !(masked && a[x] == A_NONE);
+                                cm |= ok ? (1u << x) : 0u;
+                            }
+                        }
+                    if (myq[g] >= nq) cm = 0u;
+                    const int cl = __popc(cm);
+                    int pre = 0, tot = 0;
+#pragma unroll
+                    for (int b = 0; b < 6; b++) {
+                        const unsigned long long mb_ = __ballot((cl >> b) & 1);
+                        pre += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mb_ >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mb_, 0u)) << b;
+                        tot += __popcll(mb_) << b;
+                    }
+                    unsigned base = 0;
+                    if (lane == 0) base = atomicAdd(&sy_n, (unsigned)tot);
+                    int o = __builtin_amdgcn_readfirstlane((int)base) + pre;
+                    uint4 *dst = sy_buf + (size_t)blockIdx.x * sy_wcap;
+                    if (cm != 0u) {
+#pragma unroll
+                        for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+                            for (int j = 0; j < 4; j++) {
+                                if (((cm >> (16 * bb + 4 * j)) & 15u) == 0u) continue;
+                                const knn_v4i k4 = *(const LDS_AS knn_v4i *)(cnh + (2 * (MB * rh + 2 * pr + bb) * NSEG + 16 * j));
+#pragma unroll
+                                for (int i = 0; i < 4; i++) {
+                                    const int x = 16 * bb + 4 * j + i;
+                                    if ((cm >> x) & 1u) {
+                                        // (d^2 == 0, an exact duplicate: stored as 0, dropped by the scatter)
+                                        const int d2 = qn[g] - (k4[i] >> 5) - 2 * a[x];
+                                        if (o < sy_wcap)
+                                            dst[o] = make_uint4((unsigned)(idb + 32 * (2 * pr + bb) + 8 * j + i),
+                                                                (unsigned)(d2 > 0 ? d2 : 0), (unsigned)gq[g], 0u);
+                                        o++;
                                     }
                                 }
                             }
-                        }
+                    }
                 }
             }
             // exact keys of the group (slot words from the norm ring)
@@ -205,9 +235,9 @@ def patch(s, name):
             assert s.count(old) == 1, old[:70]
             s = s.replace(old, new)
         if name == "sym_nostore":   # survivors counted, not stored (timing only)
-            old = "                                        if ((int)sl < sy_wcap)\n"
+            old = "                                        if (o < sy_wcap)\n"
             assert s.count(old) == 1
-            s = s.replace(old, "                                        if ((int)sl < 0)\n")
+            s = s.replace(old, "                                        if (o < 0)\n")
         return s
     if "noepi" in name:
         old = "            epilogue(t, acc, x);\n"

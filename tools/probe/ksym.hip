@@ -45,6 +45,7 @@ __global__ void ksym_scatter(const uint4 *buf, const unsigned *wcnt, int wcap, u
     const int n = (int)min(wcnt[w], (unsigned)wcap);
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const uint4 e = buf[(size_t)w * wcap + i];
+        if (e.y == 0u) continue;   // an exact duplicate (d^2 == 0)
         const unsigned sl = atomicAdd(ccnt + e.x, 1u);
         if ((int)sl < cap) cbuf[(size_t)e.x * cap + sl] = ((unsigned long long)e.y << 32) | e.z;
     }
