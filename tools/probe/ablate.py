@@ -264,7 +264,7 @@ def patch(s, name):
         assert old in s
         s = s.replace(old, "((t & 3) == 0)")
     if "nosum" in name:  # no cross-split summaries
-        old = "constexpr bool SUM = REREAD && KL == KNN_I8_KL_S;"
+        old = "constexpr bool SUM = REREAD && KL == KNN_I8_KL_S && QG == 1;"
         assert old in s
         s = s.replace(old, "constexpr bool SUM = false;")
     if "norr" in name:   # no shared-bound re-read (nor summaries)
