@@ -43,7 +43,7 @@ SINK = ("""            { int sk = 0;
 #pragma unroll
               for (int bb = 0; bb < MB; bb++)
 #pragma unroll
-                for (int i = 0; i < 16; i++) sk ^= acc[bb][i];
+                for (int i = 0; i < 16; i++) sk ^= acc[0][bb][i];
               if (sk == 0x12345678) part_T[0] = 1.0; }
 """)
 
@@ -83,14 +83,14 @@ def patch(s, name):
         for old, new in (
                 ("            // exact keys of the group (slot words from the norm ring)\n",
                  "            KB8C(0);\n            // exact keys of the group (slot words from the norm ring)\n"),
-                ("            int T = thr_v();\n            int vm = i8_max32(v);\n",
-                 "            KB8C(1);\n            int T = thr_v();\n            int vm = i8_max32(v);\n"),
+                ("            int T = thr_v(g);\n            int vm = i8_max32(v);\n",
+                 "            KB8C(1);\n            int T = thr_v(g);\n            int vm = i8_max32(v);\n"),
                 ("            if (__ballot(vm >= T) == 0ull) continue;\n",
                  "            if (__ballot(vm >= T) == 0ull) continue;\n            KB8C(2);\n"),
                 ("            do {\n                if (vm >= T) {\n",
                  "            do {\n                KB8C(3);\n                if (vm >= T) {\n"),
-                ("        cnt = 0;\n        refresh();\n",
-                 "        cnt = 0;\n        KB8C(4);\n        refresh();\n")):
+                ("        cnt[g] = 0;\n        refresh(g);\n",
+                 "        cnt[g] = 0;\n        KB8C(4);\n        refresh(g);\n")):
             assert old in s, old
             s = s.replace(old, new)
         return s
@@ -272,7 +272,7 @@ def patch(s, name):
         assert old in s
         s = s.replace(old, "constexpr bool REREAD = false;")
     if "filtonly" in name:   # the init-word filter only, never the keys (timing only)
-        old = "                if (__ballot(i8_max32(a) >= thr_a()) == 0ull) continue;\n"
+        old = "                if (__ballot(i8_max32(a) >= thr_a(g)) == 0ull) continue;\n"
         assert old in s
         s = s.replace(old, old + "                if (a[0] != 0x7fffffff) continue;\n")
     if "nobar" in name:
