@@ -24,6 +24,9 @@ k = 100, with m = 500000 by default (configs[4] is 4M rows on 8 GPUs; pass
 
 N > 1: one process per GPU, RCCL (torch.distributed "nccl") ring of corpus
 blocks, strong scaling (total work fixed).  Rank 0 prints one JSON line.
+Under a launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE; without one,
+--gpus N starts the N rank processes itself (launch_ranks) and exits
+non-zero when fewer than N GPUs are visible.
 """
 import argparse
 import hashlib
@@ -41,6 +44,7 @@ FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix (spec; 78.2 measured, 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix (spec, MI355X_MICROARCH.md; 155 measured)
 FP16_MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 matrix (spec ~2.5 PF, MI355X_MICROARCH.md)
 I8_MFMA_PEAK_TOPS = 5000.0      # dense int8 matrix: 2x the fp16 rate per clock (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0           # HBM3E, ~8 TB/s (MI355X_MICROARCH.md)
 
 METRIC = "all-kNN queries/sec (MNIST-784, k=30) at 1/2/4/8 GPUs + % MFMA peak"   # BASELINE.json
 
@@ -49,7 +53,8 @@ WORKLOADS = {
     "mnist": (60000, 784, 30, "f64", True,
               "all-kNN MNIST-784 k=%d (configs[1]: %dx%d fp64, leave-one-out)"),
     # configs[1] on real-valued rows (mnist_train_svd.mat is
-    # real-valued): GEMM mode, fp64 MFMA filter + exact re-rank in k_merge
+    # real-valued): GEMM mode, split-fp16 filter (k_dist_split) + exact fp64
+    # re-rank in k_merge
     "mnist-real": (60000, 784, 30, "f64", True,
                    "all-kNN MNIST-784 real-valued k=%d (configs[1] shape: %dx%d fp64, GEMM mode)"),
     "sift": (1_000_000, 128, 32, "f32", False,
@@ -79,9 +84,65 @@ def cpu_baseline(X, k, budget_s):
                       "OpenMP over queries, %.1f s)" % (q, X.shape[0], X.shape[0], X.shape[1], dt)}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n_ranks):
+    """`--gpus N` (N > 1) with no launcher around us (WORLD_SIZE unset): start
+    N rank processes of this script, torch.distributed.run-style env (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), one per GPU,
+    and return the first failing rank's exit code (0 when all succeed).  The
+    reference takes its rank count from the launch the same way
+    (mpi-knn-parallel_blocking.c:53-61: MPI_Comm_size of mpiexec -n P).
+
+    This parent touches no GPU: it only counts the devices (which does not
+    initialise HIP on this image) and refuses, with a non-zero exit, to start
+    more ranks than there are GPUs -- a P = 1 line under an n_gpus = N request
+    is never printed.  The ranks are children (no exec)."""
+    import subprocess
+    if not os.environ.get("KNN_BENCH_TEST_ENGINE"):
+        import torch
+        visible = torch.cuda.device_count()
+        if visible < n_ranks:
+            print("bench.py: --gpus %d needs %d visible GPUs, %d found; not running" % (n_ranks, n_ranks, visible),
+                  file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n_ranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n_ranks),
+                   LOCAL_WORLD_SIZE=str(n_ranks), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   KNN_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc, live = 0, list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                # a failed rank ends the job: its peers would block in the
+                # next collective until the group's timeout
+                rc = c if c > 0 else 128 - c
+                print("bench.py: rank %d exited with %d; stopping the others" % (procs.index(p), c),
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.1)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mnist")
@@ -96,11 +157,38 @@ def main():
                     help="mnist: also time the real-valued GEMM path this many steps (0: off)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus is not None and args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+        if args.gpus is not None and args.gpus < 1:
+            sys.exit("bench.py: --gpus must be >= 1")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is None:
+        args.gpus = world
+    if world != args.gpus:
+        # the line's n_gpus is the ranks that ran: never a P = 1 line for an
+        # N-GPU request, nor the reverse
+        sys.exit("bench.py: --gpus %d but the launcher started %d ranks (WORLD_SIZE)" % (args.gpus, world))
+    # KNN_BENCH_TEST_ENGINE=module:factory (tests/bench_standin.py only): a CPU
+    # stand-in engine under gloo, so the multi-rank bench path runs in the
+    # CPU test suite; the product bench always runs libknn on the GPU
+    test_engine = os.environ.get("KNN_BENCH_TEST_ENGINE")
     import torch
-    torch.cuda.set_device(local)
+    if test_engine:
+        import importlib
+        mod, attr = test_engine.split(":")
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        args.engine_factory = getattr(importlib.import_module(mod), attr)
+        backend = "gloo"
+    else:
+        args.engine_factory = None
+        backend = "nccl"
+        visible = torch.cuda.device_count()
+        if local >= visible:
+            sys.exit("bench.py: rank %d needs GPU %d, %d visible" % (rank, local, visible))
+        torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import datetime
@@ -108,9 +196,10 @@ def main():
         from mpiknn.ring import ring_timeout_s
         # a stalled or dead peer ends the run (RCCL watchdog) instead of
         # hanging it: the bound of every ring exchange (mpiknn/ring.py)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
-                                timeout=datetime.timedelta(seconds=ring_timeout_s()))
+        kw = {} if test_engine else {"device_id": torch.device("cuda", local)}
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=ring_timeout_s()), **kw)
     P = world
+    args.backend = backend if dist is not None else None
 
     res = run_workload(args.workload, args.steps, args.warmup, args, torch, dist, rank, P, local,
                        args.check, args.m, args.n, args.k)
@@ -132,7 +221,8 @@ def main():
                                      "re-rank (not the headline)",
                             "workload": sl["config"]["workload"], "value": sl["value"], "unit": sl["unit"],
                             "ms_per_step": sl["ms_per_step"], "steps": sl["steps"], "warmup": sl["warmup"],
-                            "engine": sl["engine"], "check": sl["check"], "roofline": sl["roofline"]}
+                            "engine": sl["engine"], "check": sl["check"],
+                            "check_all_rows": sl["check_all_rows"], "roofline": sl["roofline"]}
     if P == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(res["X"].astype(np.float64, copy=False), res["k"], args.cpu_seconds)
     print(json.dumps(out), flush=True)
@@ -166,23 +256,34 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         data = "synthetic (GIST-like: 256-centre mixture in [0,1), fp32)"
     R, blocks = ring.partition(m, P)
     base, rows = blocks[rank]
-    dev = torch.device("cuda", local)
+    standin = args.engine_factory is not None
+    dev = torch.device("cpu") if standin else torch.device("cuda", local)
     if layout_col:
         # own rows, column-major on the device (the .mat layout, serial:82)
         raw = torch.from_numpy(np.ascontiguousarray(X[base:base + rows].T)).to(dev).t()
     else:
         raw = torch.from_numpy(np.ascontiguousarray(X[base:base + rows])).to(dev)
-    engine = ring.GpuEngine(torch, local, n, R, rows, k, dtype=dtype)
+    if standin:
+        engine = args.engine_factory(torch, n, R, rows, k, dtype)
+    else:
+        engine = ring.GpuEngine(torch, local, n, R, rows, k, dtype=dtype)
 
     def step():
         engine.pack(raw, layout_col=layout_col)
         return ring.ring_search(dist, torch, engine, rank, P, m, base)
 
+    def sync():
+        if not standin:
+            torch.cuda.synchronize()
+
     def barrier():
-        torch.cuda.synchronize()
+        sync()
         if dist is not None:
-            dist.barrier(device_ids=[local])
-        torch.cuda.synchronize()
+            if standin:
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[local])
+        sync()
 
     last = [time.perf_counter()]
 
@@ -213,11 +314,36 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
     # record sits on the launch queues, so they stay out of ms_per_step
     prof_steps = min(steps, 5)
     engine.ctx.profile(1)
+    pack_evs = []
     for i in range(prof_steps):
-        step()
+        if standin:
+            step()
+        else:
+            # the pack runs on the caller's (torch's current) stream: timed
+            # there with torch events
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            engine.pack(raw, layout_col=layout_col)
+            e1.record()
+            pack_evs.append((e0, e1))
+            ring.ring_search(dist, torch, engine, rank, P, m, base)
         progress("profiled step %d/%d" % (i + 1, prof_steps))
     barrier()
     dist_ms, merge_ms, launches = engine.ctx.profile(0)
+    mk_ms, mk_n, mk_bytes = engine.ctx.profile_merge() if not standin else (0.0, 0, 0.0)
+    pack_ms = sum(e0.elapsed_time(e1) for e0, e1 in pack_evs) / max(len(pack_evs), 1)
+    # the pack's algorithmic bytes: the rank's rows read once in the source
+    # precision, written once as the byte block (8-bit data: round_up(n, 32)
+    # bytes + two norm words a row) or the element block (n elements + the
+    # norm)
+    es_src = raw.element_size()
+    if getattr(engine, "spec", False):
+        pack_bytes = rows * n * es_src + rows * (-(-n // 32) * 32 + 8)
+        pack_form = "byte block (k_pack8_col / k_pack8_row)"
+    else:
+        es_blk = 8 if dtype == "f64" else 4
+        pack_bytes = rows * n * es_src + rows * (n + 1) * es_blk
+        pack_form = "element block (k_pack_col / k_pack_row)"
     mode, splits = engine.ctx.info()
     cbits = engine.ctx.contraction_bits()
 
@@ -233,6 +359,26 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         mism = int((got["idx"] != ref["idx"]).sum() +
                    (got["distance"].view(np.uint64) != ref["distance"].view(np.uint64)).sum())
         check = {"queries": int(len(ref)), "mismatches": mism}
+    # every row of configs[1]/[2] (60000x784, k = 30) against the oracle's
+    # committed per-row hashes (tests/golden/*_rowhash.npz, made by
+    # tests/golden/make_golden.py): each rank hashes its own rows, the
+    # mismatch count is summed over the ranks -- at P = 8 this is the
+    # multi-GPU run's parity, every row (after the timed region)
+    all_rows = None
+    fx = {"mnist": "mnist_like", "mnist-real": "mnist_real"}.get(workload)
+    fpath = os.path.join(ROOT, "tests", "golden", "%s_rowhash.npz" % fx) if fx else None
+    if fpath and (m, n, k) == (60000, 784, 30) and os.path.exists(fpath):
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        from rowhash import row_hashes
+        with np.load(fpath, allow_pickle=False) as z:
+            want = z["hash"][base:base + rows]
+        bad = int((row_hashes(engine.result()) != want).sum()) if rows > 0 else 0
+        if dist is not None:
+            t = torch.tensor([float(bad)], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            bad = int(t.item())
+        all_rows = {"rows": m, "mismatches": bad,
+                    "fixture": "tests/golden/%s_rowhash.npz (oracle, every row)" % fx}
     if rank != 0:
         return {"line": None, "X": X, "k": k}
 
@@ -308,6 +454,32 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         "launches": launches,
         "exposed_merge_ms_per_step": merge_ms / max(prof_steps, 1),
         "profiled_steps": prof_steps,
+        # the HBM-side passes around the contraction (north_star: "achieved
+        # HBM GB/s for the top-k and norm passes"): the merge kernels (the
+        # exact fp64 re-rank / the int8 rank merge, knn_ctx_profile_merge:
+        # HIP events on the merge's stream, the engine's algorithmic byte
+        # count) and the pack / norm pass (torch events on its stream)
+        "merge": {
+            "kernel": "k_merge_rank" if cbits == 8 else "k_merge",
+            "bound": "hbm",
+            "ms_per_step": mk_ms / max(prof_steps, 1),
+            "launches_per_step": mk_n / max(prof_steps, 1),
+            "bytes_per_step": mk_bytes / max(prof_steps, 1),
+            "achieved": (mk_bytes / (mk_ms * 1e-3) / 1e9) if mk_ms > 0 else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (mk_bytes / (mk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if mk_ms > 0 else None,
+        },
+        "pack": {
+            "kernel": pack_form,
+            "bound": "hbm",
+            "ms_per_step": pack_ms,
+            "bytes_per_step": pack_bytes,
+            "achieved": (pack_bytes / (pack_ms * 1e-3) / 1e9) if pack_ms > 0 else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (pack_bytes / (pack_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if pack_ms > 0 else None,
+        },
     }
     line = {
         "metric": METRIC if workload == "mnist" else
@@ -328,9 +500,15 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         "data": data,
         "config": {"workload": wdesc % (k, m, n), "m": m, "n": n, "k": k,
                    "parallelism": "ring%d" % P},
-        "engine": {"mode": mpiknn.MODE_NAMES.get(mode, str(mode)), "splits": splits,
+        # the ranks' process group: RCCL ("nccl") across P GPUs, one process
+        # each; null at P = 1 (no collective)
+        "rccl_world": P if args.backend == "nccl" else None,
+        "launcher": os.environ.get("KNN_BENCH_LAUNCHER") or ("torch.distributed.run" if P > 1 else None),
+        "engine": {"mode": ("cpu stand-in (test only)" if standin else mpiknn.MODE_NAMES.get(mode, str(mode))),
+                   "splits": splits,
                    "unresolved_queries": unresolved},
         "check": check,
+        "check_all_rows": all_rows,
         "roofline": roofline,
         "cpu_baseline": None,
     }

@@ -422,6 +422,16 @@ KNN_API int knn_ctx_split(const knn_ctx_t *ctx);
  * k_merge work adds outside it; *launches counts k_dist_topk launches. */
 KNN_API int knn_ctx_profile(knn_ctx_t *ctx, int enable, double *dist_ms, double *merge_ms,
                     int *launches);
+/* The merge kernels' own time over the same steps (recorded while
+ * knn_ctx_profile is on): *merge_kernel_ms sums the durations of every
+ * k_merge / k_merge_rank launch (the exact fp64 re-rank of knn-serial.c:
+ * 86-91 in GEMM mode; in INT mode the rank merge, which also finalizes at
+ * the search's end), bracketed by events on the merge's stream; *merges
+ * counts them and *bytes sums their algorithmic bytes (partial lists and
+ * bounds read, state read and written or records written, and in GEMM mode
+ * the query's and its k neighbours' rows for the exact S) -- bench.py
+ * prices them against HBM. */
+KNN_API int knn_ctx_profile_merge(knn_ctx_t *ctx, double *merge_kernel_ms, int *merges, double *bytes);
 
 #ifdef __cplusplus
 }

@@ -102,12 +102,13 @@ struct knn_ctx {
     size_t q_base, q_rows_pad;
     const double *meta;
     int first_step;
+    int ended;          /* knn_ctx_end completed this search (no step since) */
     int nsplit_last;
     /* choose_splits cache: (corpus rows, list shape, kernel) -> split count;
      * a direct-exchange pass alternates two launch sizes, and one model
      * evaluation costs ~0.5 ms of host time at 15000 queries */
 #define KNN_SPLIT_CACHE 8
-    struct { size_t nc; int lpq, i8, solo, klx, best; } split_cache[KNN_SPLIT_CACHE];
+    struct { size_t nc; int lpq, i8, split, solo, klx, best; } split_cache[KNN_SPLIT_CACHE];
     int split_next;
     int nfail;
     int mode;
@@ -139,6 +140,11 @@ struct knn_ctx {
     int prof_on, prof_pending, prof_launches;
     double prof_dist_ms, prof_merge_ms;
     hipEvent_t prof_ev[3 * KNN_PROF_STEPS];
+    /* merge kernels (k_merge / k_merge_rank) alone: an event before and one
+     * after each launch on its stream (knn_ctx_profile_merge) */
+    int prof_mk_pending, prof_mk_launches;
+    double prof_mk_ms, prof_mk_bytes;
+    hipEvent_t prof_mk_ev[2 * KNN_PROF_STEPS];
 };
 
 static __thread double g_last_search_s = 0.0;
@@ -337,6 +343,8 @@ static void ctx_free_buffers(knn_ctx_t *c)
     hipFree(c->rs_i);
     for (int i = 0; i < 3 * KNN_PROF_STEPS; i++)
         if (c->prof_ev[i]) hipEventDestroy(c->prof_ev[i]);
+    for (int i = 0; i < 2 * KNN_PROF_STEPS; i++)
+        if (c->prof_mk_ev[i]) hipEventDestroy(c->prof_mk_ev[i]);
 }
 
 int knn_ctx_profile(knn_ctx_t *c, int enable, double *dist_ms, double *merge_ms, int *launches)
@@ -347,6 +355,8 @@ int knn_ctx_profile(knn_ctx_t *c, int enable, double *dist_ms, double *merge_ms,
         if (enable && !c->prof_ev[0]) {
             for (int i = 0; i < 3 * KNN_PROF_STEPS; i++)
                 HIPCHK(hipEventCreate(&c->prof_ev[i]));
+            for (int i = 0; i < 2 * KNN_PROF_STEPS; i++)
+                HIPCHK(hipEventCreate(&c->prof_mk_ev[i]));
         }
         c->prof_on = enable ? 1 : 0;
         if (enable) {
@@ -354,6 +364,10 @@ int knn_ctx_profile(knn_ctx_t *c, int enable, double *dist_ms, double *merge_ms,
             c->prof_launches = 0;
             c->prof_dist_ms = 0.0;
             c->prof_merge_ms = 0.0;
+            c->prof_mk_pending = 0;
+            c->prof_mk_launches = 0;
+            c->prof_mk_ms = 0.0;
+            c->prof_mk_bytes = 0.0;
         }
     }
     if (dist_ms) *dist_ms = c->prof_dist_ms;
@@ -401,6 +415,22 @@ static int prof_collect(knn_ctx_t *c)
     c->prof_merge_ms += all > dist ? all - dist : 0.0;
     c->prof_launches += n;
     c->prof_pending = 0;
+    for (int i = 0; i < c->prof_mk_pending; i++) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, c->prof_mk_ev[2 * i], c->prof_mk_ev[2 * i + 1]));
+        c->prof_mk_ms += ms;
+    }
+    c->prof_mk_launches += c->prof_mk_pending;
+    c->prof_mk_pending = 0;
+    return KNN_OK;
+}
+
+int knn_ctx_profile_merge(knn_ctx_t *c, double *merge_kernel_ms, int *merges, double *bytes)
+{
+    if (!c) return KNN_ERR_INVALID;
+    if (merge_kernel_ms) *merge_kernel_ms = c->prof_mk_ms;
+    if (merges) *merges = c->prof_mk_launches;
+    if (bytes) *bytes = c->prof_mk_bytes;
     return KNN_OK;
 }
 
@@ -594,6 +624,7 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
     c->q_rows_pad = knn_rows_pad(q_cap);
     c->meta = d_meta;
     c->first_step = 1;
+    c->ended = 0;
     c->nstep = 0;
     c->pend = 0;
     c->pend_nsplit = 0;
@@ -637,9 +668,8 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
     if (c->i8 && !c->sub_research && c->klx == KNN_I8_KL_S && getenv("KNN_I8_KL") && atoi(getenv("KNN_I8_KL")) == KNN_I8_KL)
         c->klx = KNN_I8_KL;
     /* 12-entry lists run on 64-row half tiles, two workgroups a CU (2 lists a
-     * query); KNN_I8_W8=1 keeps the 8-wave kernel on 128-row tiles (4) */
-    c->lpq = c->i8 ? (c->sub_research ? 2 : (c->klx == KNN_I8_KL_S && env_on("KNN_I8_W8") ? 4 : knn_i8_lpq(c->kp, c->klx)))
-                   : 4;
+     * query) */
+    c->lpq = c->i8 ? (c->sub_research ? 2 : knn_i8_lpq(c->kp, c->klx)) : 4;
     c->i8_wgpc = c->i8 && c->klx == KNN_I8_KL_S && c->lpq == 2 ? 2 : 1;
     /* fp16 shadow rows of the query block (KNN_NO_SHADOW=1: convert the
      * element fragments in the kernel instead) */
@@ -801,11 +831,26 @@ static double launch_makespan(long nqb, long ntiles, int s, int cus, double wgc)
     return ms;
 }
 
+/* remember a choose_splits result under every input it depends on */
+static int split_cache_put(knn_ctx_t *c, size_t nc, int best)
+{
+    const int e = c->split_next++ % KNN_SPLIT_CACHE;
+    c->split_cache[e].nc = nc;
+    c->split_cache[e].lpq = c->lpq;
+    c->split_cache[e].i8 = c->i8;
+    c->split_cache[e].split = c->split;
+    c->split_cache[e].solo = c->split_solo;
+    c->split_cache[e].klx = c->klx;
+    c->split_cache[e].best = best;
+    return best;
+}
+
 /* Corpus splits per query block: the count with the smallest modelled
  * launch makespan plus merge cost (each split adds a partial list per
  * query), keeping >= 4 tiles per split and the partial lists within
- * KNN_PART_BUDGET.  Cached per (corpus block size, lists a query, kernel,
- * own-block step, lane-list length): each of these changes s_min. */
+ * KNN_PART_BUDGET.  Cached per (corpus block size, lists a query, kernel
+ * -- int8, split filter (256-row tiles) or other (128-row tiles) --,
+ * own-block step, lane-list length): each of these changes the model. */
 static int choose_splits(knn_ctx_t *c, size_t nc)
 {
     const char *env = getenv("KNN_SPLITS");
@@ -813,7 +858,7 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     const long qpw = (long)KNN_TQ * (c->i8 ? knn_i8_qg(c->klx, c->lpq, c->n) : 1);
     const long nqb = (long)((c->nq + qpw - 1) / qpw);
     /* k_dist_split streams 256-row tiles: the model's tile unit is its tile */
-    const long tc = (c->split && !env_on("KNN_SPLIT_V1")) ? KNN_SPLIT_TC : KNN_TC;
+    const long tc = c->split ? KNN_SPLIT_TC : KNN_TC;
     const long ntiles = (long)((nc + tc - 1) / tc);
     /* the re-search of a few uncertified queries: one query block, so the
      * launch's span is one workgroup's scan -- as many splits as the merge
@@ -824,12 +869,16 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
     }
     if (env && atoi(env) > 0) {   /* (the search's splits, not the re-search's) */
         int s = atoi(env);
-        return s > KNN_MAX_LISTS / c->lpq ? KNN_MAX_LISTS / c->lpq : s;
+        if (s > KNN_MAX_LISTS / c->lpq) s = KNN_MAX_LISTS / c->lpq;
+        /* k_dist_split needs a tile a split (knn_launch_dist_split refuses
+         * fewer): a small block takes fewer splits than asked */
+        if (c->split && s > ntiles) s = ntiles > 0 ? (int)ntiles : 1;
+        return s;
     }
     for (int e = 0; e < KNN_SPLIT_CACHE; e++)
         if (c->split_cache[e].best > 0 && c->split_cache[e].nc == nc && c->split_cache[e].lpq == c->lpq &&
-            c->split_cache[e].i8 == c->i8 && c->split_cache[e].solo == c->split_solo &&
-            c->split_cache[e].klx == c->klx)
+            c->split_cache[e].i8 == c->i8 && c->split_cache[e].split == c->split &&
+            c->split_cache[e].solo == c->split_solo && c->split_cache[e].klx == c->klx)
             return c->split_cache[e].best;
     int smax = KNN_MAX_LISTS / c->lpq;
     const size_t per = split_bytes(c);
@@ -890,14 +939,7 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
         if (nqb * s_min < 2L * slots && s1 >= 1 && s1 < s_min &&
             (double)nc / ((double)s1 * c->lpq) <= 6000.0)
             best = (int)s1;
-        const int e = c->split_next++ % KNN_SPLIT_CACHE;
-        c->split_cache[e].nc = nc;
-        c->split_cache[e].lpq = c->lpq;
-        c->split_cache[e].i8 = c->i8;
-        c->split_cache[e].solo = c->split_solo;
-        c->split_cache[e].klx = c->klx;
-        c->split_cache[e].best = best;
-        return best;
+        return split_cache_put(c, nc, best);
     }
     for (int s = s_min; s <= smax && !short_rows; s++) {
         if (s > s_min && ntiles / s < 4) break;
@@ -907,14 +949,7 @@ static int choose_splits(knn_ctx_t *c, size_t nc)
             best_t = t;
         }
     }
-    const int e = c->split_next++ % KNN_SPLIT_CACHE;
-    c->split_cache[e].nc = nc;
-    c->split_cache[e].lpq = c->lpq;
-    c->split_cache[e].i8 = c->i8;
-    c->split_cache[e].solo = c->split_solo;
-    c->split_cache[e].klx = c->klx;
-    c->split_cache[e].best = best;
-    return best;
+    return split_cache_put(c, nc, best);
 }
 
 /* Partial lists of set `set` for nsplit splits.  Even set: the pair
@@ -970,7 +1005,7 @@ static int ensure_part_buffers(knn_ctx_t *c, int nsplit, int set, int off)
 static int rank_merge_ok(const knn_ctx_t *c, int nsplit_total)
 {
     return c->i8 && c->kp <= KNN_KP_M && (c->klx == KNN_I8_KL_S || c->klx == KNN_I8_KL) &&
-           c->lpq * nsplit_total <= 64 && !env_on("KNN_NO_RANK_MERGE");
+           c->lpq * nsplit_total <= 64;
 }
 
 /* The GEMM-mode merge reads each window candidate's element row at random
@@ -1020,8 +1055,30 @@ static int launch_merge_sets_fin(knn_ctx_t *c, int set, int nsets, int nsplit_to
                                  size_t c_base, size_t nc, knn_neighbour_t *fin_out, int *finalized)
 {
     if (finalized) *finalized = 0;
+    hipEvent_t *mk = NULL;
+    const int rank_merge = rank_merge_ok(c, nsplit_total);
+    if (c->prof_on && c->prof_mk_pending < KNN_PROF_STEPS) {
+        mk = &c->prof_mk_ev[2 * c->prof_mk_pending++];
+        HIPCHK(hipEventRecord(mk[0], c->ms));
+        /* the merge's algorithmic bytes: every partial list entry (d^2 as
+         * fp64 + idx) and bound read, the old state read and the new one
+         * written (KP x (d^2, S, idx) + 2 bounds), or with a finalizing rank
+         * merge the k records; GEMM mode adds the exact re-rank's rows --
+         * each query's row and its k neighbours' rows, the reads the
+         * reference-order S of the reported neighbours cannot avoid */
+        const double nq = (double)c->nq;
+        const double es = c->dtype == KNN_F64 ? 8.0 : 4.0;
+        double b = nq * (double)nsplit_total * ((double)c->lpq * c->klx * 12.0 + 8.0);
+        if (c->merged) b += nq * ((double)c->kp * 20.0 + 16.0);
+        b += (rank_merge && fin_out) ? nq * (double)c->k * 16.0 : nq * ((double)c->kp * 20.0 + 16.0);
+        /* (GEMM mode: the split filter's searches always; otherwise the
+         * previous search's mode, c->mode being set at knn_ctx_end) */
+        if ((c->split || c->mode == KNN_MODE_GEMM) && !rank_merge)
+            b += nq * (double)(c->k + 1) * (double)c->n * es;
+        c->prof_mk_bytes += b;
+    }
     /* int8 lists (exact INT-mode keys, k <= 32): the rank merge */
-    if (rank_merge_ok(c, nsplit_total)) {
+    if (rank_merge) {
         RCHK(knn_launch_merge_rank(c->dtype, c->kp, c->klx, c->k, c->part_d[set], c->part_i[set], c->part_T[set],
                                    nsplit_total, c->lpq, (int)c->nq, (int)c->nq_pad, !c->merged, c->st_d,
                                    c->st_x, c->st_i, c->st_T, c->qthr, fin_out, c->fail_count, c->fail_list,
@@ -1038,6 +1095,7 @@ static int launch_merge_sets_fin(knn_ctx_t *c, int set, int nsets, int nsplit_to
                               c->st_i, c->st_T, c->qblk, c->q_rows_pad, cblk, c_base, (int)nc, (int)c->n,
                               c->meta, c->qthr, c->split, perm, c->ms));
     }
+    if (mk) HIPCHK(hipEventRecord(mk[1], c->ms));
     c->merged = 1;
     /* (the search's last merge: nothing waits on its sets -- an event
      * record is one more packet on the queue before the read-back) */
@@ -1138,13 +1196,6 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     RCHK(flush_pend2(c, NULL, NULL));   /* a deferred merge goes first, in step order */
     c->split_solo = c->i8 && c->nstep == 0 && !xb && d_sblock != NULL && d_sblock == c->q8 && nc == c->nq;
     int nsplit = choose_splits(c, nc);
-    {
-        /* (diagnostic: the split count of a split-filter search's own-block
-         * step, whose merge the fused step shares) */
-        const char *os_ = getenv("KNN_OWN_SPLITS");
-        if (os_ && atoi(os_) > 0 && c->split && !xb && c->nstep == 0 && d_cblock == c->qblk)
-            nsplit = atoi(os_) < KNN_MAX_LISTS / c->lpq ? atoi(os_) : KNN_MAX_LISTS / c->lpq;
-    }
     const int set = c->nstep % KNN_PSETS, ds_i = c->nstep & 1;
     c->nsplit_last = nsplit;
     /* pairing: in exact-integer (fp16) searches two consecutive steps share
@@ -1158,8 +1209,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
      * launch anyway (every CU holds a distance workgroup; measured: the
      * merge ran on the ~20 CUs the fused launch left idle and ended after
      * it), so pairing drops a launch and its starved tail */
-    const int pair_fused = xb && c->pend && (set & 1) && c->lpq * (c->pend_nsplit + nsplit) + 1 <= 64 &&
-                           !env_on("KNN_NO_PAIR_FUSED");
+    const int pair_fused = xb && c->pend && (set & 1) && c->lpq * (c->pend_nsplit + nsplit) + 1 <= 64;
     /* a fused step (the direct exchange's received blocks) is never paired:
      * the previous step's merge runs beside it and publishes the (k+1)-th
      * d^2 of the blocks folded so far into qthr, which the fused launch's
@@ -1173,7 +1223,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
      * own block's merge could not run beside the fused launch anyway (its
      * workgroups hold every register of every CU), so it ran alone after
      * it; any other next step merges it first, as a single merge */
-    const int gemm_own = c->split && !xb && c->nstep == 0 && d_cblock == c->qblk && !env_on("KNN_NO_PAIR_FUSED");
+    const int gemm_own = c->split && !xb && c->nstep == 0 && d_cblock == c->qblk;
     int pairing = 0;
     if ((set & 1) && c->pend) {
         pairing = (can_pair && nsplit == c->pend_nsplit && !xb) || pair_fused;
@@ -1256,15 +1306,14 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
         RCHK(knn_launch_dist_i8(c->kp, c->klx, c->lpq, c->k, c->q8, c->q_rows_pad, c->q_base, (int)c->nq, &tab,
                                 knn_rows_pad(c->block_cap), (int)c->n, nsplit, c->part_d[set],
                                 c->part_i[set], c->part_T[set], (int)c->nq_pad, c->qthr,
-                                env_on("KNN_NO_QSUM") ? NULL : c->qsum, ds));
+                                c->qsum, ds));
     } else
         RCHK(knn_launch_dist_topk(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq,
                                   cblk, knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta,
                                   nsplit, c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad,
                                   c->qthr, c->split ? c->qsp : c->qsh, csh, cn_ptr,
                                   (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0) |
-                                      (c->shadow ? KNN_DIST_SHADOW : 0) | (c->split ? KNN_DIST_SPLIT : 0) |
-                                      (c->split && env_on("KNN_SPLIT_V1") ? KNN_DIST_SPLIT_V1 : 0),
+                                      (c->shadow ? KNN_DIST_SHADOW : 0) | (c->split ? KNN_DIST_SPLIT : 0),
                                   c->split ? (float)(-2.0 / ((double)c->sscale * c->sscale)) : -2.f, ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
     /* one event a step behind its distance kernel (each record is a marker
@@ -1311,6 +1360,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
         HIPCHK(hipStreamWaitEvent(cs, (c->i8 || c->h16) ? c->ev_ds[ps] : c->ev_m[ps], 0));
     }
     c->first_step = 0;
+    c->ended = 0;
     c->nstep++;
     return KNN_OK;
 }
@@ -1336,7 +1386,7 @@ int knn_ctx_step_shadow_n(knn_ctx_t *c, int nblk, const void *const *d_sblocks, 
     if (!c || nblk < 1 || !d_sblocks || !nc || !c_base || !c->shadow) return KNN_ERR_INVALID;
     for (int b = 0; b < nblk; b++)
         if (!d_sblocks[b] || nc[b] == 0 || nc[b] > c->block_cap) return KNN_ERR_INVALID;
-    if (c->shadow != 2 || env_on("KNN_NO_FUSE")) {
+    if (c->shadow != 2) {
         for (int b = 0; b < nblk; b++) RCHK(ctx_step_impl(c, NULL, d_sblocks[b], nc[b], c_base[b], NULL, stream));
         return KNN_OK;
     }
@@ -1468,6 +1518,7 @@ static int ctx_step_split_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks
     /* step s - 2 is merged by now (its merge read its blocks' rows) */
     if (c->nstep >= KNN_STEP_LAG) HIPCHK(hipStreamWaitEvent(cs, c->ev_m[(c->nstep - KNN_STEP_LAG) % KNN_PSETS], 0));
     c->first_step = 0;
+    c->ended = 0;
     c->nstep++;
     return KNN_OK;
 }
@@ -1480,7 +1531,7 @@ int knn_ctx_step_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks, const s
         if (!d_cblocks[b] || nc[b] == 0 || nc[b] > c->block_cap) return KNN_ERR_INVALID;
     /* the split filter (real-valued data, GEMM mode): fused launches of up to
      * KNN_SPLIT_MAXBLK blocks; any other contraction folds one block a step */
-    if (!c->split || env_on("KNN_NO_FUSE") || env_on("KNN_SPLIT_V1")) {
+    if (!c->split) {
         for (int b = 0; b < nblk; b++) RCHK(ctx_step_impl(c, d_cblocks[b], NULL, nc[b], c_base[b], NULL, stream));
         return KNN_OK;
     }
@@ -1627,7 +1678,8 @@ static int rescan_prep(knn_ctx_t *c, void *stream)
 int knn_ctx_research_blocks(knn_ctx_t *c, int nblk, const void *const *d_sblocks, const size_t *nc,
                             const size_t *c_base, knn_neighbour_t *d_out, size_t *unresolved, void *stream)
 {
-    if (!c || !d_out || nblk < 1 || !d_sblocks || !nc || !c_base || c->first_step) return KNN_ERR_INVALID;
+    /* only right after knn_ctx_end: nfail and fail_list are this search's */
+    if (!c || !d_out || nblk < 1 || !d_sblocks || !nc || !c_base || !c->ended) return KNN_ERR_INVALID;
     if (unresolved) *unresolved = (size_t)c->nfail;
     if (c->nfail == 0 || c->mode != KNN_MODE_INT || !c->i8 || c->shadow != 2 || c->sub_research || !c->q8 ||
         !c->have_hmeta || c->kp > KNN_KP_M || env_on("KNN_FORCE_RESCAN") || env_on("KNN_NO_RESEARCH8"))
@@ -1697,6 +1749,7 @@ static int ctx_end_merge(knn_ctx_t *c, knn_neighbour_t *d_out)
 int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *stream)
 {
     if (!c || !d_out || c->first_step) return KNN_ERR_INVALID;
+    c->ended = 0;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
     /* The last merge, finalize and the counter read-back run behind the
@@ -1722,7 +1775,7 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
     HIPCHK(hipEventRecord(c->ev_in, s));
     HIPCHK(hipEventSynchronize(c->ev_in));
     hipStream_t ms = c->ms;
-    if (!c->merged && c->nstep >= 1 && !env_on("KNN_END_ON_MS")) {
+    if (!c->merged && c->nstep >= 1) {
         const int last = (c->nstep - 1) & 1;
         if (c->nstep >= 2) HIPCHK(hipEventSynchronize(c->ev_ds[(c->nstep - 2) % KNN_PSETS]));
         c->ms = c->ds[last];
@@ -1748,7 +1801,9 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
         (void)hipGetLastError();
     }
     if (unresolved) *unresolved = (size_t)c->nfail;
-    return rescan_prep(c, stream);
+    RCHK(rescan_prep(c, stream));
+    c->ended = 1;
+    return KNN_OK;
 }
 
 int knn_ctx_rescan_step(knn_ctx_t *c, const void *d_cblock, size_t nc, size_t c_base,

@@ -144,8 +144,6 @@ int knn_launch_dist_topk(int dtype, int kp, int k, const void *qblk, size_t q_ro
 #define KNN_DIST_SHADOW 4  /* with H16: stage the fp16 shadow rows qsh / csh      */
 #define KNN_DIST_SPLIT  8  /* fp32 blocks: split fp16 filter on the split shadow rows
                               qsh / csh (knn_launch_shadow_split); m2s = -2 / S^2   */
-#define KNN_DIST_SPLIT_V1 16 /* with SPLIT: k_dist_topk's 128-row-tile form instead of
-                                k_dist_split (KNN_SPLIT_V1=1; A/B runs)            */
 /* k_dist_split (knn_split.hip): the split fp16 filter on 256-row tiles,
  * over up to KNN_SPLIT_MAXBLK corpus blocks in one launch (block b: split
  * rows sp[b], norms nrm[b] of its element block, global ids base[b].., nc[b]

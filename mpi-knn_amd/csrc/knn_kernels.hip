@@ -163,8 +163,7 @@ __device__ __forceinline__ double knn_cert_E(int n, double qn, double maxnorm, i
     if (split) {
         const double ul = 5.9604644775390625e-08;   // 2^-24
         // the n/32 chunk sums are added in fp32 (k_dist_split, fp32 and fp64
-        // blocks alike; k_dist_topk's KNN_SPLIT_V1 form adds fp64 blocks' in
-        // fp64, within this)
+        // blocks alike)
         const double acc = (double)n / 25.0;
         return ((136.0 + acc) * ul + 4.0 * nn * 1.1102230246251565e-16) * qc * (1.0 + 1e-6) +
                1.4901161193847656e-08 * maxabs * sqrt((double)n) * (sqrt(qn) + sqrt(maxnorm));
@@ -529,19 +528,17 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
     const T *__restrict__ cblk, const T *__restrict__ cnorm, size_t c_base, int nc,
     int n, int n_pad, int ntiles, int nsplit, int nqb, const double *__restrict__ meta,
     double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T,
-    int nq_pad, unsigned long long *__restrict__ qthr, int uj, int xord, float m2s)
+    int nq_pad, unsigned long long *__restrict__ qthr, int uj, int xord)
 {
     constexpr int NST = KNN_NST;
     // H16 2: qblk / cblk are fp16 shadow rows (k_shadow), n_pad their row
-    // length; the norms stay in the element blocks
-    // H16 3: split fp16 shadow rows (knn_shadow_split, 4 bytes a feature:
-    // per 32 features 32 hi halves then 32 lo halves); fp64 blocks keep
-    // their fp64 accumulators (in the fp32 MFMA layout)
-    constexpr int RS = H16 == 2 ? 2 : (H16 == 3 ? 4 : (int)sizeof(T));   // bytes per staged element
+    // length; the norms stay in the element blocks.  (Split fp16 rows have a
+    // kernel of their own, k_dist_split in knn_split.hip.)
+    constexpr int RS = H16 == 2 ? 2 : (int)sizeof(T);   // bytes per staged element
     constexpr int BK = 128 / RS;                      // features per 128-B chunk
     // fp64 H16 (knn_to_h4): the fp32 MFMA output layout, row 4g + r of a
     // 16-row m-tile in lane group g, register r, instead of fp64's g + 4r
-    constexpr bool H16D = H16 != 0 && H16 != 3 && sizeof(T) == 8;
+    constexpr bool H16D = H16 != 0 && sizeof(T) == 8;
     constexpr bool F32L = H16 != 0 && sizeof(T) == 8;   // fp64 accumulators, fp32 MFMA layout
     auto rowmap = [](int gg, int r) { return F32L ? 4 * gg + r : KT<T>::row(gg, r); };
     constexpr int ES = (int)sizeof(T);
@@ -727,7 +724,7 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
             for (int m4 = 0; m4 < 4; m4++)
 #pragma unroll
                 for (int r = 0; r < 4; r++)
-                    A[4 * hh + m4][r] = fma(H16 == 3 ? (T)m2s : (T)-2, A[4 * hh + m4][r], qn + cnr[m4][r]);
+                    A[4 * hh + m4][r] = fma((T)-2, A[4 * hh + m4][r], qn + cnr[m4][r]);
         }
         T lanemin = A[0][0];
 #pragma unroll
@@ -896,37 +893,6 @@ __global__ __launch_bounds__(512, 2) void k_dist_topk(
                     }
                     if constexpr (H16D) {
                         if (++grp == 4) flush32();
-                    }
-                    advance();
-                    __builtin_amdgcn_s_waitcnt(0xC07F);
-                    if constexpr (SELF) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                    __builtin_amdgcn_s_barrier();
-                    glds1(0);
-                    continue;
-                }
-                if constexpr (H16 == 3) {
-                    // split fp16: slot g of the chunk row holds the hi
-                    // halves of features 8g..8g+7 of the 32, slot 4+g their
-                    // lo halves; hi.hi + hi.lo + lo.hi (knn_cert_E, split)
-                    glds1(1);
-                    glds1(2);
-                    glds1(3);
-                    const knn_h8 qh = *(const LDS_AS knn_h8 *)(cs + 16384 + wave * 2048 + fslot);
-                    const knn_h8 ql = *(const LDS_AS knn_h8 *)(cs + 16384 + wave * 2048 + fslot1);
-#pragma unroll
-                    for (int mt = 0; mt < 8; mt++) {
-                        const knn_h8 ah = *(const LDS_AS knn_h8 *)(cs + mt * 2048 + fslot);
-                        const knn_h8 al = *(const LDS_AS knn_h8 *)(cs + mt * 2048 + fslot1);
-                        // a chunk's 96 products summed apart (cross terms
-                        // first), then added to the accumulator: its rounding
-                        // runs over n/32 chunk sums, not 3n products
-                        // (knn_cert_E, split); fp64 blocks add them in fp64
-                        flt4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ql, (flt4){0, 0, 0, 0}, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, qh, t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qh, t, 0, 0, 0);
-#pragma unroll
-                        for (int r = 0; r < 4; r++) acc[mt][r] += (T)t[r];
                     }
                     advance();
                     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -2399,23 +2365,15 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
         // split fp16 shadow rows (4 bytes a feature); m2s = -2 / S^2 undoes
         // the scaling in the epilogue's fma (a power of two: exact)
         if (!qsh || !csh) return KNN_ERR_INVALID;
-        if (!(flags & KNN_DIST_SPLIT_V1)) {
-            knn_split_blocks_t cb{};
-            cb.nblk = 1;
-            cb.sp[0] = csh;
-            cb.nrm[0] = cnorm;
-            cb.base[0] = (int64_t)c_base;
-            cb.nc[0] = nc;
-            cb.lim[0] = (int)c_rows_pad;
-            return knn_launch_dist_split(dt, KL, qsh, qnorm, q_base, nq, &cb, n, meta, nsplit, part_d, part_i, part_T,
-                                         nq_pad, qthr, uj, xord, m2s, s);
-        }
-        const int nps = (int)knn_round_up((size_t)n, 32);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 3>), grid, dim3(512), 0, s,
-                           (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
-                           nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                           (unsigned long long *)qthr, uj, xord, m2s);
-        return hip_status();
+        knn_split_blocks_t cb{};
+        cb.nblk = 1;
+        cb.sp[0] = csh;
+        cb.nrm[0] = cnorm;
+        cb.base[0] = (int64_t)c_base;
+        cb.nc[0] = nc;
+        cb.lim[0] = (int)c_rows_pad;
+        return knn_launch_dist_split(dt, KL, qsh, qnorm, q_base, nq, &cb, n, meta, nsplit, part_d, part_i, part_T,
+                                     nq_pad, qthr, uj, xord, m2s, s);
     }
     if ((flags & KNN_DIST_SHADOW) && (flags & KNN_DIST_H16)) {
         if (!qsh || !csh) return KNN_ERR_INVALID;
@@ -2428,12 +2386,12 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 2>), grid, dim3(512), 0, s,
                                (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
                                nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                               (unsigned long long *)qthr, uj, xord, -2.f);
+                               (unsigned long long *)qthr, uj, xord);
         else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 1, 2>), grid, dim3(512), 0, s,
                                (const T *)qsh, qnorm, q_base, nq, (const T *)csh, cnorm, c_base, nc, n,
                                nps, ntiles, nsplit, nqb, meta, part_d, part_i, part_T, nq_pad,
-                               (unsigned long long *)qthr, uj, xord, -2.f);
+                               (unsigned long long *)qthr, uj, xord);
         return hip_status();
     }
     {
@@ -2441,13 +2399,13 @@ static int launch_dist_topk(const T *qblk, size_t q_rows_pad, size_t q_base, int
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP, 0, 1>), grid, dim3(512), 0, s,
                                qblk, qnorm, q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles, nsplit,
                                nqb, meta, part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr,
-                               uj, xord, -2.f);
+                               uj, xord);
             return hip_status();
         }
     }
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_topk<T, KL, KP>), grid, dim3(512), 0, s, qblk, qnorm,
                        q_base, nq, cblk, cnorm, c_base, nc, n, np, ntiles, nsplit, nqb, meta, part_d,
-                       part_i, part_T, nq_pad, (unsigned long long *)qthr, uj, xord, -2.f);
+                       part_i, part_T, nq_pad, (unsigned long long *)qthr, uj, xord);
     return hip_status();
 }
 

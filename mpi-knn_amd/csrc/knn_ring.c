@@ -236,7 +236,21 @@ static int ring_drain(ring_dev_t *d, int P, ring_transport_t *t, int comm, int *
                 bad = 1;
         }
         if (!pending && !bad) {
-            for (int g = 0; g < P; g++) d[g].nmk = 0;   /* every mark has completed */
+            /* the polled streams are idle; marks recorded on the other kind
+             * of stream (compute or comm) may still be pending: keep those
+             * (swapped to the front, so no event is lost) and drop only the
+             * completed ones, so a later drain still counts their progress */
+            for (int g = 0; g < P; g++) {
+                if (hipSetDevice(d[g].dev) != hipSuccess) return KNN_ERR_HIP;
+                int keep = 0;
+                for (int x = 0; x < d[g].nmk; x++)
+                    if (hipEventQuery(d[g].mk[x]) != hipSuccess) {
+                        hipEvent_t e = d[g].mk[keep];
+                        d[g].mk[keep++] = d[g].mk[x];
+                        d[g].mk[x] = e;
+                    }
+                d[g].nmk = keep;
+            }
             return KNN_OK;
         }
         const int now_marks = ring_marks_done(d, P);

@@ -450,345 +450,6 @@ __global__ __launch_bounds__(512) void k_dist_split(
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_dist_split32: the same filter on v_mfma_f32_32x32x16_f16 (lists of <= 24
-// entries: fp64 k <= 32, fp32 k <= 32).  The 16x16 form reads a 1 KiB A
-// fragment from LDS for every 8K multiply-adds; its ablations (mnist-real,
-// DESIGN.md sec.4.6) put the fragment reads, the MFMAs and the LDS-DMA
-// writes one after the other rather than side by side -- the LDS array is
-// the shared resource.  A 32x32x16 fragment feeds 16K multiply-adds: half
-// the LDS read bytes for the same work.
-//
-//   wave w: query group qg = w & 3 (32 queries), row half rh = w >> 2; lane
-//   l = 32 h + r supplies A row R = r / B query r with halves [8h, 8h + 8)
-//   of each 16-feature K-step -- 16-byte segments h, 2 + h (hi) and 4 + h,
-//   6 + h (lo) of the 128-byte chunk row.  A row R of the wave's m-block b
-//   (b < 4) is tile row 64 b + 16 (R >> 3) + 8 rh + (R & 7), so D register i
-//   of m-block b holds tile row 64 b + 16 (i >> 2) + 8 rh + 4 h + (i & 3)
-//   for query r: list 2 rh + h sees the rows 4 (2 rh + h) .. +3 mod 16, the
-//   same share as a lane group of the 16x16 form, so a run of consecutive
-//   rows (a cluster stored together) spreads evenly over the four lists.
-//   (Contiguous row halves a wave put 40 clustered rows on the two lanes of
-//   one wave, 20 a 16-entry list: 877 of 2050 queries of the near-tie test
-//   went uncertified; alternating 32-row m-blocks still left 31.)  A query's 4 lists: lanes h = 0, 1 of the two
-//   row-half waves (lpq = 4, list 2 rh + h); bounds shared by the two lanes
-//   of a wave.
-//   LDS image: segment s of tile row R at slot s ^ sw32(R), sw32(R) = bits
-//   1, 2, 4 of R (each 16-lane group of a fragment read -- rows 8 rh + 0..7
-//   and 16 + 8 rh + 0..7 of a 32-row group -- hits 16 distinct bank quads);
-//   norms ring [rh][h][b][j][i] (the lane's 64 rows contiguous).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int sw32(int row) { return ((row >> 1) & 3) | ((row >> 2) & 4); }
-
-template <typename T, int KL>
-__global__ __launch_bounds__(512) void k_dist_split32(
-    const char *__restrict__ qsp, const T *__restrict__ qnorm, size_t q_base, int nq,
-    const knn_split_blocks_t cb, int n, int rsb, int nsplit, int nqb, const double *__restrict__ meta,
-    double *__restrict__ part_d, int *__restrict__ part_i, double *__restrict__ part_T, int nq_pad,
-    unsigned long long *__restrict__ qthr, int uj, int xord, float m2s)
-{
-    constexpr int ES = (int)sizeof(T);
-    __shared__ __attribute__((aligned(16))) char smem[SP_LDS];
-    LDS_AS char *lds = (LDS_AS char *)smem;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r32 = lane & 31, h = lane >> 5;
-    const int wave_s = __builtin_amdgcn_readfirstlane(wave);
-    const int qg = wave_s & 3, rh = wave_s >> 2;
-    int qb, split;
-    if (xord) {
-        const int slot = blockIdx.x >> 3;
-        split = slot % nsplit;
-        qb = ((slot / nsplit) << 3) + (blockIdx.x & 7);
-        if (qb >= nqb) return;
-    } else {
-        qb = blockIdx.x % nqb;
-        split = blockIdx.x / nqb;
-    }
-    const int ntiles = cb.t0[cb.nblk];
-    auto blk_of = [&](int t) {
-        int b = 0;
-#pragma unroll
-        for (int j = 1; j < KNN_SPLIT_MAXBLK; j++) b = (j < cb.nblk && t >= cb.t0[j]) ? j : b;
-        return b;
-    };
-    const int tb = ntiles / nsplit, tr = ntiles - tb * nsplit;
-    const int t_lo = split * tb + (split < tr ? split : tr);
-    const int t_hi = t_lo + tb + (split < tr ? 1 : 0);
-    const int mode = knn_mode<T>(meta, n);
-    const int qrow0 = qb * SP_TQ;
-    const int myq = qrow0 + 32 * qg + r32;
-    const long gq = (long)q_base + myq;
-    const float qn = (float)qnorm[myq];
-    asm volatile("" ::"v"(qn));
-    const int nfc = rsb / 128;
-    const int ujm = (mode == KNN_MODE_INT) ? (uj & 255) : (uj >> 8);
-
-    float L[KL];
-    int I[KL];
-#pragma unroll
-    for (int e = 0; e < KL; e++) { L[e] = __builtin_inff(); I[e] = -1; }
-    float thr = __builtin_inff();
-    if (qthr != nullptr && myq < nq)
-        thr = sp_bound_up(__longlong_as_double((long long)atomicMin(qthr + myq, 0x7ff0000000000000ull)));
-    if (myq >= nq) thr = -__builtin_inff();
-    asm volatile("" ::"v"(thr));
-    const int total = (mode == KNN_MODE_SCAN || t_hi <= t_lo) ? 0 : (t_hi - t_lo) * nfc;
-
-    typedef float knn_f16v __attribute__((ext_vector_type(16)));
-    knn_f16v acc[4];
-#pragma unroll
-    for (int b = 0; b < 4; b++)
-#pragma unroll
-        for (int i = 0; i < 16; i++) acc[b][i] = 0.f;
-
-    // ---- staging: wave w stages tile rows 32 w .. +31 (4 pieces of 8 rows)
-    const int lr = lane >> 3, ls = lane & 7;
-    int s_c = 0, s_t = t_lo, s_fc = 0, s_st = 0;
-    int s_b = blk_of(t_lo);
-    const char *s_row = (const char *)cb.sp[s_b] + (size_t)(t_lo - cb.t0[s_b]) * SP_TC * rsb;
-    int s_lim = cb.lim[s_b] - 1 - (t_lo - cb.t0[s_b]) * SP_TC;
-    int s_next = s_b + 1 < cb.nblk ? cb.t0[s_b + 1] : 0x7fffffff;
-    auto glds1 = [&](int i) {
-        const unsigned dst0 = (unsigned)(uintptr_t)lds + (unsigned)s_st * SP_STAGE;
-        const char *cp = s_row + (size_t)128 * s_fc;
-        const int row = 32 * wave_s + 8 * i + lr;                   // tile row
-        const int lrow = row < s_lim ? row : s_lim;
-        bglds16(knn_rsrc(cp), (unsigned)(lrow * rsb + 16 * (ls ^ sw32(row))),
-                dst0 + (unsigned)(32 * wave_s + 8 * i) * 128u);
-    };
-    auto advance = [&]() {
-        s_c++;
-        s_st = s_st == SP_NST - 1 ? 0 : s_st + 1;
-        if (s_c < total) {
-            if (++s_fc == nfc) {
-                s_fc = 0;
-                if (++s_t == s_next) {
-                    s_b++;
-                    s_row = (const char *)cb.sp[s_b];
-                    s_lim = cb.lim[s_b] - 1;
-                    s_next = s_b + 1 < cb.nblk ? cb.t0[s_b + 1] : 0x7fffffff;
-                } else {
-                    s_row += (size_t)SP_TC * rsb;
-                    s_lim -= SP_TC;
-                }
-            }
-        }
-    };
-    // query fragments straight into registers (as k_dist_split): segments
-    // h, 2 + h, 4 + h, 6 + h of the lane's query row, one chunk ahead
-    const char *qrow = qsp + (size_t)myq * rsb + 16 * h;
-    auto bload = [&](int fc, knn_si4 (&q)[4]) {
-        const char *p = qrow + (size_t)128 * fc;
-        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(q[0]) : "v"(p) : "memory");
-        asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(q[1]) : "v"(p) : "memory");
-        asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(q[2]) : "v"(p) : "memory");
-        asm volatile("global_load_dwordx4 %0, %1, off offset:96" : "=v"(q[3]) : "v"(p) : "memory");
-    };
-    // norm slice of tile t into ring slot t & 3, [rh][h][b][j][i]
-    constexpr int NU = SP_TC * ES / 4;
-    auto gnorm = [&](int t) {
-        if (wave_s >= NU / 64) return;
-        const int ts = t < t_hi ? t : t_hi - 1;
-        const int bk = blk_of(ts);
-        const int u = 64 * wave_s + lane;
-        const int p = ES == 8 ? u >> 1 : u;
-        const int prh = p >> 7, ph = (p >> 6) & 1, pb = (p >> 4) & 3, pj = (p >> 2) & 3, pi = p & 3;
-        int row = (ts - cb.t0[bk]) * SP_TC + 64 * pb + 16 * pj + 8 * prh + 4 * ph + pi;
-        row = row < cb.lim[bk] ? row : cb.lim[bk] - 1;
-        const char *src = (const char *)((const T *)cb.nrm[bk] + row) + (ES == 8 ? (u & 1) * 4 : 0);
-        glds4(src, (unsigned)(uintptr_t)lds + SP_NORM_OFF + (unsigned)(t & 3) * SP_NORM_SLOT +
-                       (unsigned)wave_s * 256u);
-    };
-
-    auto epilogue = [&](int t) {
-        const LDS_AS T *cng = (const LDS_AS T *)(lds + SP_NORM_OFF + (t & 3) * SP_NORM_SLOT) + 64 * (2 * rh + h);
-        const float lim = L[KL - 1] < thr ? L[KL - 1] : thr;
-        const int eb = blk_of(t);
-        const long c_base = cb.base[eb];
-        const int nc = cb.nc[eb];
-        const int tr0 = (t - cb.t0[eb]) * SP_TC;                    // the tile's first row
-        const int row0 = tr0 + 8 * rh;                               // the wave's first row
-        const long gt0 = (long)c_base + tr0, gw0 = (long)q_base + qrow0 + 32 * qg;
-        const bool masked = (tr0 + SP_TC > nc) || (gw0 < gt0 + SP_TC && gt0 < gw0 + 32);
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                float cn[4];
-                if constexpr (ES == 8) {
-                    const dbl2 n01 = ((const LDS_AS dbl2 *)cng)[2 * (4 * b + j)];
-                    const dbl2 n23 = ((const LDS_AS dbl2 *)cng)[2 * (4 * b + j) + 1];
-                    cn[0] = (float)n01.x; cn[1] = (float)n01.y; cn[2] = (float)n23.x; cn[3] = (float)n23.y;
-                } else {
-                    const flt4 n4 = ((const LDS_AS flt4 *)cng)[4 * b + j];
-                    cn[0] = n4.x; cn[1] = n4.y; cn[2] = n4.z; cn[3] = n4.w;
-                }
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    acc[b][4 * j + i] = __builtin_fmaf(m2s, acc[b][4 * j + i], qn + cn[i]);
-            }
-        float lanemin = acc[0][0];
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-#pragma unroll
-            for (int i = (b == 0 ? 1 : 0); i < 16; i++) lanemin = fminf(lanemin, acc[b][i]);
-        const bool any = masked || __ballot(lanemin <= lim) != 0ull;
-        if (any) {
-            const float zfloor = (mode == KNN_MODE_INT) ? 0.f : -__builtin_inff();
-            // bit 16 b + i: row 64 b + 16 (i >> 2) + 4 h + (i & 3) (+ row0), rising with the bit
-            unsigned long long pend = 0;
-#pragma unroll
-            for (int b = 0; b < 4; b++)
-#pragma unroll
-                for (int i = 0; i < 16; i++) pend |= (acc[b][i] <= lim) ? (1ull << (16 * b + i)) : 0ull;
-            if (masked) {
-#pragma unroll
-                for (int b = 0; b < 4; b++)
-#pragma unroll
-                    for (int i = 0; i < 16; i++) {
-                        const int row = row0 + 64 * b + 16 * (i >> 2) + 4 * h + (i & 3);
-                        if (!(row < nc && (long)c_base + row != gq)) pend &= ~(1ull << (16 * b + i));
-                    }
-            }
-            while (__ballot(pend != 0) != 0ull) {
-                const int bit = pend ? __builtin_ctzll(pend) : 0;
-                const bool b0 = bit & 1, b1 = bit & 2, b2 = bit & 4, b3 = bit & 8, b4 = bit & 16, b5 = bit & 32;
-                float v[4];
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    // (named temporaries: an array here became a scratch table)
-                    const float w0 = b0 ? acc[b][1] : acc[b][0], w1 = b0 ? acc[b][3] : acc[b][2];
-                    const float w2 = b0 ? acc[b][5] : acc[b][4], w3 = b0 ? acc[b][7] : acc[b][6];
-                    const float w4 = b0 ? acc[b][9] : acc[b][8], w5 = b0 ? acc[b][11] : acc[b][10];
-                    const float w6 = b0 ? acc[b][13] : acc[b][12], w7 = b0 ? acc[b][15] : acc[b][14];
-                    const float x0 = b1 ? w1 : w0, x1 = b1 ? w3 : w2, x2 = b1 ? w5 : w4, x3 = b1 ? w7 : w6;
-                    const float y0 = b2 ? x1 : x0, y1 = b2 ? x3 : x2;
-                    v[b] = b3 ? y1 : y0;
-                }
-                const float z0 = b4 ? v[1] : v[0], z1 = b4 ? v[3] : v[2];
-                const float dsel = b5 ? z1 : z0;
-                const float dd = (pend && dsel > zfloor) ? dsel : __builtin_inff();
-                const int i = bit & 15;
-                const int ii = (int)(c_base + row0 + 64 * (bit >> 4) + 16 * (i >> 2) + 4 * h + (i & 3));
-                pend &= pend - 1;
-                list_insert<KL>(L, I, dd, ii);
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-#pragma unroll
-            for (int i = 0; i < 16; i++) acc[b][i] = 0.f;
-        if (!any) return;
-        // the wave's two lanes of the query
-        float lmin = L[KL - 1], u = L[0];
-#pragma unroll
-        for (int e = 1; e < KL; e++) u = (e == ujm) ? L[e] : u;
-        lmin = fminf(lmin, __shfl_xor(lmin, 32));
-        u = fmaxf(u, __shfl_xor(u, 32));
-        thr = fminf(thr, fminf(lmin, u));
-    };
-
-    // fragment of segment s (0..7) of the wave's m-block b (tile row 64 b + frow)
-    const int frow = 16 * (r32 >> 3) + 8 * rh + (r32 & 7);   // sw32 does not depend on b
-    const int fsw = sw32(frow);
-    auto rdA = [&](const LDS_AS char *cs, int b, int sgm) {
-        return *(const LDS_AS knn_sh8 *)(cs + (frow + 64 * b) * 128 + 16 * (sgm ^ fsw));
-    };
-
-    if (total > 0) {
-        knn_si4 q_c[4], q_n[4];
-        bload(0, q_c);
-        gnorm(t_lo);
-        gnorm(t_lo + 1);
-#pragma unroll
-        for (int x = 0; x < SP_NST - 1; x++) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) glds1(i);
-            advance();
-        }
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-#pragma unroll
-        for (int x = 0; x < 4; x++) asm volatile("" : "+v"(q_c[x]));
-        __builtin_amdgcn_s_barrier();
-
-        int st = 0, fcq = 0;
-        for (int t = t_lo; t < t_hi; t++) {
-            gnorm(t + 2);
-            for (int fc = 0; fc < nfc; fc++) {
-                LDS_AS char *cs = lds + st * SP_STAGE;
-                fcq = fcq + 1 == nfc ? 0 : fcq + 1;
-                bload(fcq, q_n);
-                const knn_sh8 qh0 = __builtin_bit_cast(knn_sh8, q_c[0]), qh1 = __builtin_bit_cast(knn_sh8, q_c[1]);
-                const knn_sh8 ql0 = __builtin_bit_cast(knn_sh8, q_c[2]), ql1 = __builtin_bit_cast(knn_sh8, q_c[3]);
-                // A fragments two m-blocks ahead: [slot][hi0, hi1, lo0, lo1]
-                knn_sh8 a[2][4];
-#pragma unroll
-                for (int b = 0; b < 2; b++)
-#pragma unroll
-                    for (int x = 0; x < 4; x++) a[b][x] = rdA(cs, b, 2 * x + h);
-                knn_f16v tt[2];
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const int sl = b & 1;
-                    knn_f16v x = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[sl][0], ql0, (knn_f16v){}, 0, 0, 0);
-                    x = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[sl][1], ql1, x, 0, 0, 0);
-                    x = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[sl][2], qh0, x, 0, 0, 0);
-                    x = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[sl][3], qh1, x, 0, 0, 0);
-                    x = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[sl][0], qh0, x, 0, 0, 0);
-                    tt[sl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[sl][1], qh1, x, 0, 0, 0);
-                    if (b + 2 < 4) {
-#pragma unroll
-                        for (int x2 = 0; x2 < 4; x2++) a[sl][x2] = rdA(cs, b + 2, 2 * x2 + h);
-                    }
-                    if (b > 0) acc[b - 1] += tt[(b - 1) & 1];
-                    glds1(b);
-                    if (b == 3) advance();
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                acc[3] += tt[1];
-                __builtin_amdgcn_s_waitcnt(0xC07F);
-                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-#pragma unroll
-                for (int x = 0; x < 4; x++) {
-                    asm volatile("" : "+v"(q_n[x]));
-                    q_c[x] = q_n[x];
-                }
-                __builtin_amdgcn_s_barrier();
-                st = st == SP_NST - 1 ? 0 : st + 1;
-            }
-            epilogue(t);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-
-    float lastmin = L[KL - 1];
-    lastmin = fminf(lastmin, __shfl_xor(lastmin, 32));
-    float pub = thr;
-    if (mode == KNN_MODE_INT && lastmin > thr && thr < __builtin_inff()) pub = nextafterf(thr, __builtin_inff());
-    // T of the query: min over its two row-half waves (LDS: the norm ring is free now)
-    {
-        float *xd = (float *)(smem + SP_NORM_OFF);
-        __syncthreads();
-        if (h == 0 && rh == 1) xd[32 * qg + r32] = pub;
-        __syncthreads();
-        if (rh == 0) {
-            const float po = xd[32 * qg + r32];
-            pub = po < pub ? po : pub;
-        }
-    }
-    if (myq < nq) {
-        const size_t base = (((size_t)split * nq_pad + myq) * 4 + 2 * rh + h) * KL;
-#pragma unroll
-        for (int e = 0; e < KL; e++) {
-            part_d[base + e] = (double)L[e];
-            part_i[base + e] = I[e];
-        }
-        if (h == 0 && rh == 0) part_T[(size_t)split * nq_pad + myq] = (double)pub;
-        if (h == 0 && qthr != nullptr && thr < __builtin_inff())
-            atomicMin(qthr + myq, (unsigned long long)__double_as_longlong((double)thr));
-    }
-}
-
 template <typename T, int KL, int D>
 static int launch_split(const void *qsp, const T *qnorm, size_t q_base, int nq, const knn_split_blocks_t &cb, int n,
                         const double *meta, int nsplit, double *part_d, int *part_i, double *part_T, int nq_pad,
@@ -797,17 +458,9 @@ static int launch_split(const void *qsp, const T *qnorm, size_t q_base, int nq, 
     const int rsb = (int)knn_split_rs((size_t)n);
     const int nqb = (nq + SP_TQ - 1) / SP_TQ;
     const int nqb_grid = xord ? (nqb + 7) / 8 * 8 : nqb;
-    // k_dist_split32 is opt-in (KNN_SPLIT32=1): mnist-real 21.7 ms a launch
-    // against the 16x16 form's 17.0 (tools/r05_s11.sh)
-    const char *e32 = getenv("KNN_SPLIT32");
-    if (KL <= 24 && e32 && e32[0] == '1')
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_split32<T, KL <= 24 ? KL : 24>), dim3((unsigned)(nqb_grid * nsplit)),
-                           dim3(512), 0, s, (const char *)qsp, qnorm, q_base, nq, cb, n, rsb, nsplit, nqb, meta,
-                           part_d, part_i, part_T, nq_pad, (unsigned long long *)qthr, uj, xord, m2s);
-    else
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_split<T, KL, D>), dim3((unsigned)(nqb_grid * nsplit)), dim3(512), 0,
-                           s, (const char *)qsp, qnorm, q_base, nq, cb, n, rsb, nsplit, nqb, meta, part_d, part_i,
-                           part_T, nq_pad, (unsigned long long *)qthr, uj, xord, m2s);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_dist_split<T, KL, D>), dim3((unsigned)(nqb_grid * nsplit)), dim3(512), 0, s,
+                       (const char *)qsp, qnorm, q_base, nq, cb, n, rsb, nsplit, nqb, meta, part_d, part_i, part_T,
+                       nq_pad, (unsigned long long *)qthr, uj, xord, m2s);
     return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
 }
 

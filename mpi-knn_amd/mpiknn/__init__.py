@@ -48,7 +48,7 @@ API_SYMBOLS = (
     "knn_ctx_shadow", "knn_ctx_step_shadow", "knn_ctx_begin_meta", "knn_ctx_shadow_bytes",
     "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n", "knn_ctx_split", "knn_s8_block_bytes",
     "knn_s8_block_meta_offset", "knn_block_pack_s8", "knn_s8_spec_ok", "knn_ctx_begin_s8",
-    "knn_ctx_attach_qblock", "knn_ctx_research_blocks", "knn_ctx_step_n",
+    "knn_ctx_attach_qblock", "knn_ctx_research_blocks", "knn_ctx_step_n", "knn_ctx_profile_merge",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -124,6 +124,7 @@ def _load():
         "knn_ctx_step_shadow": ([p, p, sz, sz, p], i),
         "knn_ctx_step_shadow_n": ([p, i, pp, psz, psz, p], i),
         "knn_ctx_profile": ([p, i, ctypes.POINTER(d), ctypes.POINTER(d), ctypes.POINTER(i)], i),
+        "knn_ctx_profile_merge": ([p, ctypes.POINTER(d), ctypes.POINTER(i), ctypes.POINTER(d)], i),
         "knn_s8_block_bytes": ([sz, sz], sz),
         "knn_s8_block_meta_offset": ([sz, sz], sz),
         "knn_block_pack_s8": ([p, i, sz, sz, sz, p, i, sz, i, p], i),
@@ -443,6 +444,14 @@ class Context:
         _check(lib.knn_ctx_profile(self._h, enable, ctypes.byref(dm), ctypes.byref(mm),
                                    ctypes.byref(n)), "knn_ctx_profile")
         return dm.value, mm.value, n.value
+
+    def profile_merge(self):
+        """knn_ctx_profile_merge: (merge kernel ms, merge launches,
+        algorithmic bytes) over the profiled steps."""
+        mm, n, b = ctypes.c_double(), ctypes.c_int(), ctypes.c_double()
+        _check(lib.knn_ctx_profile_merge(self._h, ctypes.byref(mm), ctypes.byref(n), ctypes.byref(b)),
+               "knn_ctx_profile_merge")
+        return mm.value, n.value, b.value
 
     def info(self):
         mode, splits = ctypes.c_int(), ctypes.c_int()

@@ -21,9 +21,15 @@ hold, so the GPU tests can check neighbour lists against committed data:
                       (i32), d2 (u32, exact integers);
 * mnist_real_sample.npz  datasets.mnist_real(60000) (real-valued, the GEMM
                       mode): the same 48 rows, k=30: rows, idx (i32), the
-                      distances' raw fp64 bits (u64).
+                      distances' raw fp64 bits (u64);
+* mnist_like_rowhash.npz / mnist_real_rowhash.npz  EVERY row of the two
+                      60000x784 corpora (configs[1]/[2]): a 64-bit hash per
+                      row of its k=30 (idx i32 LE, distance fp64 bits LE)
+                      record (row_hashes(); SURVEY sec.4's "sampled rows plus
+                      per-row hashes"), so the GPU tests compare all 60000
+                      rows, not only the 48 sampled ones.
 
-  python tests/golden/make_golden.py [--only mnist_real]
+  python tests/golden/make_golden.py [--only mnist_real|rowhash]
 """
 import json
 import os
@@ -33,10 +39,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.dirname(HERE)]
+sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.dirname(HERE), HERE]
 
 import datasets  # noqa: E402
 import oracle  # noqa: E402
+from rowhash import row_hashes  # noqa: E402  (the same hash the tests take)
 
 REFERENCE_RUNS = {
     "_source": "SURVEY.md sec.0 (F1, F7) and sec.4: reference binaries run on these inputs",
@@ -74,9 +81,23 @@ def mnist_real_fixture():
                         dist_bits=bits)
 
 
+def rowhash_fixtures():
+    """the oracle's all-kNN of every row of both 60000x784 corpora (a few
+    minutes each on the container's cores), kept as per-row hashes"""
+    for name, make in (("mnist_like", datasets.mnist_like), ("mnist_real", datasets.mnist_real)):
+        X, _ = make(60000)
+        nb = oracle.knn(X, 30)
+        np.savez_compressed(os.path.join(HERE, "%s_rowhash.npz" % name), k=np.int32(30),
+                            m=np.int32(60000), hash=row_hashes(nb))
+        print("wrote", name, flush=True)
+
+
 def main():
     if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "mnist_real":
         mnist_real_fixture()
+        return
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "rowhash":
+        rowhash_fixtures()
         return
     with open(os.path.join(HERE, "reference_runs.json"), "w") as f:
         json.dump(REFERENCE_RUNS, f, indent=1)
@@ -109,6 +130,7 @@ def main():
         d2[i] = exact_s(nb["distance"][0])
     np.savez_compressed(os.path.join(HERE, "mnist_like_sample.npz"), rows=rows, idx=idx, d2=d2)
     mnist_real_fixture()
+    rowhash_fixtures()
     print("golden fixtures written to", HERE)
 
 

@@ -8,8 +8,10 @@ once (the reference visits r, r-2, ..., r-P), so each rank's
 rows must carry the serial lists of knn-serial.c:72-93:
 
 * mnist_like(60000) x 784 (configs[2]) and its real-valued form (fp64 GEMM
-  mode, element blocks on the wire): the 48 committed golden rows bit for
-  bit, and all 60000 rows byte-identical to the one-GPU search;
+  mode, element blocks on the wire): all 60000 rows against the oracle's
+  committed per-row hashes, the 48 golden rows bit for bit, and the whole
+  result byte-identical to the one-GPU search; the integer form once more
+  with every transfer through RCCL (self-loop communicator);
 * a SIFT-shaped 1M x 128 fp32 corpus (configs[3]): 16 rows spread over the
   eight ranks against the oracle's scan.
 
@@ -21,7 +23,7 @@ import numpy as np
 import pytest
 
 import datasets
-from test_golden import check_mnist_rows, load
+from test_golden import check_all_rows, check_mnist_rows, load
 from test_gpu_parity import assert_same
 
 pytestmark = pytest.mark.gpu
@@ -42,8 +44,20 @@ def test_mnist_full_size_p8_loopback(knn, monkeypatch, schedule):
     monkeypatch.setenv("KNN_RING_SCHEDULE", schedule)
     nb, _ = knn.search(Xf, 30, ngpus=8, layout="col")
     check_mnist_rows(nb[load("mnist_like_sample.npz")["rows"]], load("mnist_like_sample.npz"))
+    check_all_rows(nb, "mnist_like")
     _props(nb, 60000)
     assert nb.tobytes() == one.tobytes(), "P=8 %s differs from the one-GPU search" % schedule
+
+
+def test_mnist_full_size_p8_rccl_self(knn, monkeypatch):
+    """configs[2] at full size with every transfer through RCCL (the
+    one-device self-loop communicator of knn_ring.c, P = 8 virtual ranks):
+    all 60000 rows against the oracle's per-row hashes"""
+    X, _ = datasets.mnist_like(60000)
+    monkeypatch.setenv("KNN_RING_LOOPBACK", "rccl")
+    monkeypatch.setenv("KNN_RING_SCHEDULE", "direct")
+    nb, _ = knn.search(np.asfortranarray(X), 30, ngpus=8, layout="col")
+    check_all_rows(nb, "mnist_like")
 
 
 def test_mnist_real_full_size_p8_loopback(knn, monkeypatch):
@@ -56,6 +70,7 @@ def test_mnist_real_full_size_p8_loopback(knn, monkeypatch):
     g = load("mnist_real_sample.npz")
     assert np.array_equal(nb[g["rows"]]["idx"], g["idx"])
     assert np.array_equal(nb[g["rows"]]["distance"].view(np.uint64), g["dist_bits"])
+    check_all_rows(nb, "mnist_real")
     _props(nb, 60000)
     assert nb.tobytes() == one.tobytes()
 

@@ -26,6 +26,10 @@ with  KB8_SO=tools/probe/abl/libkbench8_<name>.so python tools/probe/kbench8.py
                direction on the tiles past the block's own: per-row
                thresholds w = lim - |r'|^2 staged as the (unused, long-row)
                init words, survivors appended to a per-workgroup region
+  stagA_D / stagB_D  the product kernel with the first round's second-slot
+               (A: blockIdx 256..511; B: odd XCD-local ids) workgroups
+               started D x 1024 cycles late (an epilogue stagger between
+               the two workgroups of a CU; timing only)
   count        the product kernel plus per-wave event counters (one vector
                atomic a wave and event, lane 0): groups past the init-word
                filter (all groups where it is off), groups whose exact keys
@@ -63,6 +67,21 @@ STAMP_HDR = """__device__ unsigned long long kb8_stamp[4 * 16384];
 
 
 def patch(s, name):
+    if name.startswith("stag"):
+        # stagA_D: the first round's second-slot workgroups (blockIdx 256..511:
+        # breadth-first dispatch puts them beside 0..255 on the 256 CUs) start
+        # D x 1024 cycles late, so the two workgroups of a CU -- and every
+        # later pair, which inherits the offset through the freed slots --
+        # reach their epilogues at different times; stagB_D: the odd
+        # XCD-local workgroups of the first round instead (depth-first
+        # placement: b and b + 8 on one CU).  Timing only; results unchanged.
+        kind, d = name[4], int(name.split("_")[1])
+        cond = ("(blockIdx.x >= 256u && blockIdx.x < 512u)" if kind == "A"
+                else "(blockIdx.x < 512u && ((blockIdx.x >> 3) & 1u))")
+        old = "    const int qb = blockIdx.x % nqb, split = blockIdx.x / nqb;\n"
+        assert s.count(old) == 1
+        s = s.replace(old, old + "    if (%s) { for (int z_ = 0; z_ < %d; z_++) __builtin_amdgcn_s_sleep(16); }\n" % (cond, d))
+        return s
     if name == "stamp":
         # per-workgroup wall clock (100 MHz): start, first chunk ready, loop
         # done, end -- kbench8.py prints the spans of the last timed launch
