@@ -214,3 +214,29 @@ def test_rccl_ring_driver_one_gpu(knn, oracle, monkeypatch):
         for p in sorted({1, ng}):
             got, _ = knn.search(X, 30, ngpus=p, layout="col")
             assert_same(got, ref, "rccl ring P=%d" % p)
+
+
+@pytest.mark.parametrize("what", ["fp64-int-no-i8", "real-split", "fp32-sift", "real-no-split"])
+def test_xcd_grouped_order(knn, oracle, monkeypatch, what):
+    """KNN_XCD_ORDER=1: the XCD-grouped workgroup order of k_dist_topk and
+    k_dist_split (the split-major order is the default)
+    gives the same lists -- the order only moves which workgroup folds which
+    (query block, split), never the result (knn-serial.c:72-93)."""
+    monkeypatch.setenv("KNN_XCD_ORDER", "1")
+    if what == "fp64-int-no-i8":
+        monkeypatch.setenv("KNN_NO_I8", "1")
+        X = datasets.mnist_like(2000, 784, seed=21)[0]
+        got, _ = knn.search(X, 30)
+        ref = oracle.knn(X, 30)
+    elif what in ("real-split", "real-no-split"):
+        if what == "real-no-split":
+            monkeypatch.setenv("KNN_NO_SPLIT", "1")
+        X = datasets.digits_real()[0]
+        got, _ = knn.search(X, 30)
+        ref = oracle.knn(X, 30)
+    else:
+        monkeypatch.setenv("KNN_NO_I8", "1")
+        X = datasets.sift_like(4000, 128)
+        got, _ = knn.search(X, 32, dtype="f32")
+        ref = oracle.knn(X.astype(np.float32).astype(np.float64), 32)
+    assert_same(got, ref, "xcd order %s" % what)
