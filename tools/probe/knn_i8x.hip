@@ -9,7 +9,11 @@
 // SIMD (256 VGPRs) the 13- and 14-step instantiations spill 37-63 VGPRs
 // (the 4- and 8-step ones fit).  The probe's clock gain (tools/probe/
 // i8_shape_probe.hip) needs a layout that keeps the query fragments in
-// fewer registers first.
+// fewer registers first.  Also tried: reloading the last NK - 8 steps' query
+// fragments from L2 every tile (this file's NRES / reload()): 64-77 spilled
+// VGPRs -- the pressure peak is the tile loop itself (query fragments,
+// accumulators, the next tile's first A fragments and both groups' lists),
+// not the epilogue.
 // knn_i8x.hip -- the int8 contraction on v_mfma_i32_16x16x64_i8: the k <= 31
 // default for rows of more than 4 K-steps (MNIST's n = 784).
 //
@@ -131,13 +135,24 @@ __global__ __launch_bounds__(256, 2) void k_dist_topk_i8x(
 
     // ---- resident query fragments: step k, lane (g4, j16) = bytes
     // [64 k + 16 g4, +16) of its query row (zero past the row) ----------------
-    knn_v4i qf[2][NK];
+    // The first NRES steps stay resident; the last NRL are loaded again
+    // every tile (from L2: each wave re-reads its own 32 rows), issued at
+    // chunk CI's last step ahead of its stage and waited for at their first
+    // use in chunk CU: resident, all NK steps took 104 of the 256 VGPRs a
+    // wave has at two waves a SIMD, and the two groups' epilogue state
+    // spilled 37-63 VGPRs (tools/r06_s3.sh)
+    constexpr int NRES = NK < 8 ? NK : 8;
+    constexpr int NRL = NK - NRES;
+    constexpr int CU = NRES / 2, CI = CU - 3;
+    static_assert(NRL == 0 || (CI >= 0 && NRES % 2 == 0), "reload schedule");
+    knn_v4i qf[2][NRES];
+    knn_v4i qr[2][NRL > 0 ? NRL : 1];
     int qn[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
         const signed char *qrow = qsh + (size_t)lq[s] * rs + 16 * g4;
 #pragma unroll
-        for (int k = 0; k < NK; k++) {
+        for (int k = 0; k < NRES; k++) {
             const bool in = 64 * k + 16 * g4 < rs;
             const knn_v4i v = *(const knn_v4i *)(qrow + (in ? 64 * k : 0));
             qf[s][k] = in ? v : (knn_v4i){0, 0, 0, 0};
@@ -244,6 +259,32 @@ __global__ __launch_bounds__(256, 2) void k_dist_topk_i8x(
                                16 * ((4 * ks2 + g4) ^ aswz);
         return *(const LDS_AS knn_v4i *)p;
     };
+
+    // reloaded query fragments: asm loads (invisible to the compiler's wait
+    // pass, as the ring's), so the stage()s issued after them are younger:
+    // 3 stages x 2 pieces by chunk CU, where vmcnt(6) sees them landed
+    auto reload = [&]() {
+#pragma unroll
+        for (int s = 0; s < 2; s++)
+#pragma unroll
+            for (int j = 0; j < NRL; j++) {
+                const int k = NRES + j;
+                const signed char *p = qsh + (size_t)lq[s] * rs + 16 * g4 + (64 * k + 16 * g4 < rs ? 64 * k : 0);
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qr[s][j]) : "v"(p) : "memory");
+            }
+    };
+    auto reload_ready = [&]() {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+#pragma unroll
+        for (int s = 0; s < 2; s++)
+#pragma unroll
+            for (int j = 0; j < NRL; j++) {
+                asm volatile("" : "+v"(qr[s][j]));
+                if (64 * (NRES + j) + 16 * g4 >= rs) qr[s][j] = (knn_v4i){0, 0, 0, 0};   // past the row
+            }
+    };
+    // the query fragment of K-step k (static after unrolling)
+    auto qfrag = [&](int s, int k) -> knn_v4i { return k < NRES ? qf[s][k < NRES ? k : 0] : qr[s][k >= NRES ? k - NRES : 0]; };
 
     // ---- bounds (k_dist_topk_i8: every value bounds the query's (k+1)-th
     // d^2 over all rows, or is the lane's own KL-th) ------------------------
@@ -410,11 +451,13 @@ __global__ __launch_bounds__(256, 2) void k_dist_topk_i8x(
                         // before its first fragments are read
                         const bool last = ks2 + 1 >= kt;
                         const bool more = !last || x + 1 < total;
+                        if (NRL > 0 && c == CI && last) reload();
                         if (last && x + 1 < total) {
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x + 1)
                             stage();
                         }
+                        if (NRL > 0 && 2 * c + ks2 == NRES) reload_ready();
 #if I8X_PF
                         // the next step's 4 fragments first, then this step's MFMAs
                         knn_v4i an[4];
@@ -424,16 +467,16 @@ __global__ __launch_bounds__(256, 2) void k_dist_topk_i8x(
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                         for (int mt = 0; mt < 4; mt++) {
-                            acc[0][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mt], qf[0][2 * c + ks2], acc[0][mt], 0, 0, 0);
-                            acc[1][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mt], qf[1][2 * c + ks2], acc[1][mt], 0, 0, 0);
+                            acc[0][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mt], qfrag(0, 2 * c + ks2), acc[0][mt], 0, 0, 0);
+                            acc[1][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mt], qfrag(1, 2 * c + ks2), acc[1][mt], 0, 0, 0);
                         }
 #pragma unroll
                         for (int mt = 0; mt < 4; mt++) a[mt] = an[mt];
 #else
 #pragma unroll
                         for (int mt = 0; mt < 4; mt++) {
-                            acc[0][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mt], qf[0][2 * c + ks2], acc[0][mt], 0, 0, 0);
-                            acc[1][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mt], qf[1][2 * c + ks2], acc[1][mt], 0, 0, 0);
+                            acc[0][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mt], qfrag(0, 2 * c + ks2), acc[0][mt], 0, 0, 0);
+                            acc[1][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mt], qfrag(1, 2 * c + ks2), acc[1][mt], 0, 0, 0);
                             // the next step's fragment of this m-tile into the slot
                             if (more) a[mt] = last ? rdA1(xs + 1 == NST ? 0 : xs + 1, 0, mt) : rdA1(xs, ks2 + 1, mt);
                             __builtin_amdgcn_sched_barrier(0);
