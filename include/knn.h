@@ -433,6 +433,19 @@ KNN_API int knn_ctx_profile(knn_ctx_t *ctx, int enable, double *dist_ms, double 
  * prices them against HBM. */
 KNN_API int knn_ctx_profile_merge(knn_ctx_t *ctx, double *merge_kernel_ms, int *merges, double *bytes);
 
+/* on != 0: the context's searches fold ONE block in one step (a P = 1
+ * search, knn-serial.c:72-93 over the whole corpus): the step's distance
+ * kernel and knn_ctx_end's merge run on the caller's stream, back to back,
+ * with no event record or cross-stream wait between them, and end() does
+ * not wait for the caller's stream on the host first.  A second step in such
+ * a search falls back to the step schedule (exact either way).  Default 0. */
+KNN_API int knn_ctx_set_solo(knn_ctx_t *ctx, int on);
+/* The 8 meta doubles the last search's kernels read (copied to mapped host
+ * memory by its last kernel; valid after knn_ctx_end returned KNN_OK): a
+ * caller that began the search from a meta hint checks it with this,
+ * without a read-back copy of its own on the stream. */
+KNN_API int knn_ctx_search_meta(const knn_ctx_t *ctx, double *meta);
+
 #ifdef __cplusplus
 }
 #endif

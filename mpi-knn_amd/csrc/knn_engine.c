@@ -103,6 +103,11 @@ struct knn_ctx {
     const double *meta;
     int first_step;
     int ended;          /* knn_ctx_end completed this search (no step since) */
+    /* knn_ctx_set_solo: a search of one step runs its distance kernel and
+     * merge on the caller's stream (solo_on: this search's first step did,
+     * ms_keep holds the merge stream meanwhile) */
+    int solo, solo_on;
+    hipStream_t ms_keep;
     int nsplit_last;
     /* choose_splits cache: (corpus rows, list shape, kernel) -> split count;
      * a direct-exchange pass alternates two launch sizes, and one model
@@ -425,6 +430,21 @@ static int prof_collect(knn_ctx_t *c)
     return KNN_OK;
 }
 
+int knn_ctx_set_solo(knn_ctx_t *c, int on)
+{
+    if (!c) return KNN_ERR_INVALID;
+    c->solo = on ? 1 : 0;
+    return KNN_OK;
+}
+
+int knn_ctx_search_meta(const knn_ctx_t *c, double *meta)
+{
+    if (!c || !meta || !c->ended) return KNN_ERR_INVALID;
+    const volatile double *m = (const volatile double *)((const char *)c->h_count + 16);
+    for (int i = 0; i < KNN_META_DOUBLES; i++) meta[i] = m[i];
+    return KNN_OK;
+}
+
 int knn_ctx_profile_merge(knn_ctx_t *c, double *merge_kernel_ms, int *merges, double *bytes)
 {
     if (!c) return KNN_ERR_INVALID;
@@ -478,7 +498,10 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     ok &= hipMalloc((void **)&c->fail_list, np * sizeof(int)) == hipSuccess;
     ok &= hipMalloc((void **)&c->fbound, np * sizeof(double)) == hipSuccess;
     if (ok) c->mode_dev = c->fail_count + 1;
-    ok &= hipHostMalloc((void **)&c->h_count, 2 * sizeof(int), hipHostMallocMapped) == hipSuccess;
+    /* mapped: [0] unresolved, [1] mode, then (at byte 16) the search's 8
+     * meta doubles as its kernels read them (knn_ctx_search_meta) */
+    ok &= hipHostMalloc((void **)&c->h_count, 16 + KNN_META_DOUBLES * sizeof(double), hipHostMallocMapped) ==
+          hipSuccess;
     ok &= c->h_count && hipHostGetDevicePointer((void **)&c->h_count_dev, c->h_count, 0) == hipSuccess;
     for (int b = 0; b < 2; b++) {
         ok &= hipStreamCreateWithFlags(&c->ds[b], hipStreamNonBlocking) == hipSuccess;
@@ -625,6 +648,10 @@ static int ctx_begin(knn_ctx_t *c, const void *d_qblock, const void *d_s8, size_
     c->meta = d_meta;
     c->first_step = 1;
     c->ended = 0;
+    if (c->solo_on) {   /* (a search abandoned before its end) */
+        c->ms = c->ms_keep;
+        c->solo_on = 0;
+    }
     c->nstep = 0;
     c->pend = 0;
     c->pend_nsplit = 0;
@@ -1242,8 +1269,29 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
     }
     const void *cblk = d_cblock;
     hipStream_t cs = (hipStream_t)stream, ds = c->ds[ds_i];
-    HIPCHK(hipEventRecord(c->ev_in, cs));
-    HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
+    if (c->solo_on) {
+        /* a second step after a solo first one: back to the step schedule
+         * (step 0's kernel ran on the caller's stream; its merge is pending
+         * and will run on the merge stream) */
+        HIPCHK(hipEventRecord(c->ev_ds[0], (hipStream_t)c->ms));
+        HIPCHK(hipStreamWaitEvent(c->ms_keep, c->ev_ds[0], 0));
+        c->ms = c->ms_keep;
+        c->solo_on = 0;
+    }
+    /* a solo search (one block, one step: P = 1): the distance kernel on the
+     * caller's stream, its merge behind it there -- no event record or
+     * stream wait between pack, kernel and merge (each a queue packet of
+     * 5-20 us, rocprofv3) */
+    const int solo = c->solo && c->nstep == 0 && !xb;
+    if (solo) {
+        ds = cs;
+        c->ms_keep = c->ms;
+        c->ms = cs;
+        c->solo_on = 1;
+    } else {
+        HIPCHK(hipEventRecord(c->ev_in, cs));
+        HIPCHK(hipStreamWaitEvent(ds, c->ev_in, 0));
+    }
     if (c->nstep >= KNN_PSETS) HIPCHK(hipStreamWaitEvent(ds, c->ev_m[set], 0));
     const void *csh = d_sblock, *cn_ptr = NULL;
     if (c->i8) {
@@ -1321,8 +1369,10 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
      * merge stream, the caller's lag wait and knn_ctx_end all use ev_ds.
      * (The distance kernel waited for ev_in: ev_ds covers the block's
      * arrival too -- a second wait would add its own latency) */
-    HIPCHK(hipEventRecord(c->ev_ds[set], ds));
-    HIPCHK(hipStreamWaitEvent(c->ms, c->ev_ds[set], 0));
+    if (!solo) {
+        HIPCHK(hipEventRecord(c->ev_ds[set], ds));
+        HIPCHK(hipStreamWaitEvent(c->ms, c->ev_ds[set], 0));
+    }
     if (pairing) {
         /* the pending even step (step s - 1, on the other distance stream) */
         HIPCHK(hipStreamWaitEvent(c->ms, c->ev_ds[(set + KNN_PSETS - 1) % KNN_PSETS], 0));
@@ -1739,7 +1789,8 @@ static int ctx_end_merge(knn_ctx_t *c, knn_neighbour_t *d_out)
                                  c->fail_list, c->mode_dev, c->fbound, env_on("KNN_FORCE_RESCAN"),
                                  c->split, c->ms));
     c->h_count[0] = c->h_count[1] = -1;
-    RCHK(knn_launch_count_out(c->fail_count, c->h_count_dev, c->ms));
+    RCHK(knn_launch_count_out(c->fail_count, c->h_count_dev, c->meta,
+                              (double *)((char *)c->h_count_dev + 16), c->ms));
     /* the host waits for the results, so the caller's stream needs no wait
      * packet on them (one would sit before that stream's next kernel) */
     HIPCHK(hipStreamSynchronize(c->ms));
@@ -1772,16 +1823,28 @@ int knn_ctx_end(knn_ctx_t *c, knn_neighbour_t *d_out, size_t *unresolved, void *
      * that completed long before (rocprofv3, P = 1: distance kernel -> 24 us
      * -> merge on the same queue, with only the caller-stream wait between).
      * Nothing on the caller's stream can wait on work end() enqueues. */
-    HIPCHK(hipEventRecord(c->ev_in, s));
-    HIPCHK(hipEventSynchronize(c->ev_in));
+    /* A solo search's kernel and merge are on the caller's stream already
+     * (knn_ctx_set_solo): nothing to wait for on the host, the merge follows
+     * the kernel there. */
     hipStream_t ms = c->ms;
-    if (!c->merged && c->nstep >= 1) {
-        const int last = (c->nstep - 1) & 1;
-        if (c->nstep >= 2) HIPCHK(hipEventSynchronize(c->ev_ds[(c->nstep - 2) % KNN_PSETS]));
-        c->ms = c->ds[last];
+    if (c->solo_on) {
+        if ((hipStream_t)stream != c->ms) {   /* end() on another stream than the step's */
+            HIPCHK(hipEventRecord(c->ev_in, c->ms));
+            HIPCHK(hipStreamWaitEvent(s, c->ev_in, 0));
+            c->ms = s;
+        }
+    } else {
+        HIPCHK(hipEventRecord(c->ev_in, s));
+        HIPCHK(hipEventSynchronize(c->ev_in));
+        if (!c->merged && c->nstep >= 1) {
+            const int last = (c->nstep - 1) & 1;
+            if (c->nstep >= 2) HIPCHK(hipEventSynchronize(c->ev_ds[(c->nstep - 2) % KNN_PSETS]));
+            c->ms = c->ds[last];
+        }
     }
     const int rc_end = ctx_end_merge(c, d_out);
-    c->ms = ms;
+    c->ms = c->solo_on ? c->ms_keep : ms;
+    c->solo_on = 0;
     RCHK(rc_end);
     RCHK(prof_collect(c));
     c->nfail = ((volatile int *)c->h_count)[0];

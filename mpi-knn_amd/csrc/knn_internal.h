@@ -203,8 +203,9 @@ int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const double *part_d
                           const double *meta, int n, int force_fail, void *stream);
 /* qthr = +inf, qsum (may be NULL) = empty summaries, counts[0..1] = 0 */
 int knn_launch_begin_init(double *qthr, unsigned long long *qsum, int nq_pad, int *counts, void *stream);
-/* counts[0..1] -> mapped host memory (k_count_out) */
-int knn_launch_count_out(const int *d_count, int *mapped, void *stream);
+/* counts[0..1] -> mapped host memory, and the meta (8 doubles; NULL: none)
+ * -> mapped_meta (k_count_out) */
+int knn_launch_count_out(const int *d_count, int *mapped, const double *meta, double *mapped_meta, void *stream);
 /* split fp16 shadow rows of an fp32 / fp64 block: per 32 features 32 halves hi =
  * RN16(S x), then 32 halves lo = RN16(S x - hi); rows of round_up(n, 32) * 4
  * bytes; S a power of two (knn_engine.c: maxabs S in [2^13, 2^14)) */

@@ -1974,16 +1974,20 @@ __global__ void k_begin_init(double *qthr, unsigned long long *qsum, int nq_pad,
     if (i < 2) counts[i] = 0;
 }
 
-// the search's (unresolved, mode) pair into mapped host memory (knn_ctx_end
-// reads it after synchronising with the stream)
-__global__ void k_count_out(const int *__restrict__ src, int *__restrict__ dst)
+// the search's (unresolved, mode) pair and the meta its kernels read into
+// mapped host memory (knn_ctx_end reads them after synchronising with the
+// stream; the meta is knn_ctx_search_meta's -- no separate read-back copy)
+__global__ void k_count_out(const int *__restrict__ src, int *__restrict__ dst, const double *__restrict__ meta,
+                            double *__restrict__ dst_meta)
 {
     if (threadIdx.x < 2) dst[threadIdx.x] = src[threadIdx.x];
+    if (meta != nullptr && threadIdx.x < KNN_META_DOUBLES) dst_meta[threadIdx.x] = meta[threadIdx.x];
 }
 
-extern "C" int knn_launch_count_out(const int *d_count, int *mapped, void *stream)
+extern "C" int knn_launch_count_out(const int *d_count, int *mapped, const double *meta, double *mapped_meta,
+                                    void *stream)
 {
-    hipLaunchKernelGGL(k_count_out, dim3(1), dim3(64), 0, (hipStream_t)stream, d_count, mapped);
+    hipLaunchKernelGGL(k_count_out, dim3(1), dim3(64), 0, (hipStream_t)stream, d_count, mapped, meta, mapped_meta);
     return hipGetLastError() == hipSuccess ? KNN_OK : KNN_ERR_HIP;
 }
 

@@ -49,6 +49,7 @@ API_SYMBOLS = (
     "knn_ctx_shadow_pack", "knn_ctx_step_shadow_n", "knn_ctx_split", "knn_s8_block_bytes",
     "knn_s8_block_meta_offset", "knn_block_pack_s8", "knn_s8_spec_ok", "knn_ctx_begin_s8",
     "knn_ctx_attach_qblock", "knn_ctx_research_blocks", "knn_ctx_step_n", "knn_ctx_profile_merge",
+    "knn_ctx_set_solo", "knn_ctx_search_meta",
 )
 DTYPES = {"f64": F64, "f32": F32, F64: F64, F32: F32}
 
@@ -125,6 +126,8 @@ def _load():
         "knn_ctx_step_shadow_n": ([p, i, pp, psz, psz, p], i),
         "knn_ctx_profile": ([p, i, ctypes.POINTER(d), ctypes.POINTER(d), ctypes.POINTER(i)], i),
         "knn_ctx_profile_merge": ([p, ctypes.POINTER(d), ctypes.POINTER(i), ctypes.POINTER(d)], i),
+        "knn_ctx_set_solo": ([p, i], i),
+        "knn_ctx_search_meta": ([p, ctypes.POINTER(d)], i),
         "knn_s8_block_bytes": ([sz, sz], sz),
         "knn_s8_block_meta_offset": ([sz, sz], sz),
         "knn_block_pack_s8": ([p, i, sz, sz, sz, p, i, sz, i, p], i),
@@ -444,6 +447,16 @@ class Context:
         _check(lib.knn_ctx_profile(self._h, enable, ctypes.byref(dm), ctypes.byref(mm),
                                    ctypes.byref(n)), "knn_ctx_profile")
         return dm.value, mm.value, n.value
+
+    def set_solo(self, on):
+        """knn_ctx_set_solo: one-step searches (P = 1) on the caller's stream."""
+        _check(lib.knn_ctx_set_solo(self._h, 1 if on else 0), "knn_ctx_set_solo")
+
+    def search_meta(self):
+        """knn_ctx_search_meta: the meta the last search's kernels read."""
+        out = (ctypes.c_double * META_DOUBLES)()
+        _check(lib.knn_ctx_search_meta(self._h, out), "knn_ctx_search_meta")
+        return np.frombuffer(out, dtype=np.float64).copy()
 
     def profile_merge(self):
         """knn_ctx_profile_merge: (merge kernel ms, merge launches,

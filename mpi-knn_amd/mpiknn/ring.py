@@ -305,6 +305,11 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
     if schedule not in ("ring", "direct"):
         raise ValueError("unknown ring schedule %r" % (schedule,))
     R, blocks = partition(m, P)
+    ctx = getattr(engine, "ctx", None)
+    if ctx is not None and hasattr(ctx, "set_solo"):
+        # P = 1 folds one block in one step: kernel and merge on the caller's
+        # stream, no cross-stream events (knn_ctx_set_solo)
+        ctx.set_solo(P == 1)
     wire = False
     h_meta = None
     verify = None
@@ -485,11 +490,18 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
     else:
         one_pass(0, False)
     if verify is True:
-        # the meta's read-back, enqueued behind the steps: on the caller's
-        # stream it would sit between the pack and the search's first kernel
-        # (a 6 us copy on the critical path); end() waits for it
-        verify = engine.meta_host(engine.meta)
+        if P == 1 and hasattr(ctx, "search_meta"):
+            # the search's last kernel copies the meta it read into mapped
+            # memory (knn_ctx_search_meta): no read-back copy on the stream
+            verify = "search_meta"
+        else:
+            # the meta's read-back, enqueued behind the steps: on the
+            # caller's stream it would sit between the pack and the search's
+            # first kernel (a 6 us copy on the critical path); end() waits
+            verify = engine.meta_host(engine.meta)
     unresolved = engine.end()
+    if isinstance(verify, str):
+        verify = ctx.search_meta()
     if (unresolved > 0 and held_s and P > 1 and hasattr(engine, "research") and engine.ctx.shadow() == 2):
         # a ring rank's uncertified queries: searched again on the int8
         # contraction (65-entry lists) over the byte blocks it holds, before
@@ -499,7 +511,8 @@ def ring_search(dist, torch, engine, rank, P, m, q_base, schedule=None, timeout_
     if verify is not None and P == 1:
         # (the read-back was enqueued on the caller's stream before end(),
         # which waits for that stream: it has landed)
-        if not engine.mk.s8_spec_ok(verify.numpy(), engine.n, engine.dtype):
+        if not engine.mk.s8_spec_ok(verify.numpy() if hasattr(verify, "numpy") else np.asarray(verify),
+                                    engine.n, engine.dtype):
             engine.spec_hint = None   # not this data: the checked path, from the start
             return ring_search(dist, torch, engine, rank, P, m, q_base, schedule, timeout_s)
     if verify is not None and P > 1:
