@@ -59,12 +59,11 @@ __device__ __forceinline__ void glds4(const void *src, unsigned lds_dst)
 //   GEMM: everything else.
 // ---------------------------------------------------------------------------
 template <typename T>
-__device__ __forceinline__ int knn_mode(const double *meta, int n)
+__device__ __forceinline__ int knn_mode_lim(const double *meta, int n, double lim)
 {
     if constexpr (sizeof(T) == 8) {
         if (meta[KNN_META_NONFINITE] != 0.0 || !(meta[KNN_META_MAXNORM] < 1e290))
             return KNN_MODE_SCAN;
-        const double lim = 2251799813685248.0 / (4.0 * (double)n);   // 2^51 / 4n
         double mx = meta[KNN_META_MAXABS];
         if (meta[KNN_META_NONINT] == 0.0 && mx * mx <= lim) return KNN_MODE_INT;
         return KNN_MODE_GEMM;
@@ -78,6 +77,14 @@ __device__ __forceinline__ int knn_mode(const double *meta, int n)
             return KNN_MODE_INT;
         return KNN_MODE_GEMM;
     }
+}
+// lim = 2^51 / 4n (fp64 INT-mode limit on max|x|^2), the same correctly
+// rounded quotient on the host or here; a caller with many waves passes the
+// host's (k_merge_rank: no fp64 division a wave)
+template <typename T>
+__device__ __forceinline__ int knn_mode(const double *meta, int n)
+{
+    return knn_mode_lim<T>(meta, n, 2251799813685248.0 / (4.0 * (double)n));
 }
 
 // ---------------------------------------------------------------------------

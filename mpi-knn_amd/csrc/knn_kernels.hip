@@ -1395,6 +1395,7 @@ struct knn_fin_args {
     int *fail_count, *fail_list, *mode_out;
     double *fbound;
     const double *meta;
+    double lim;   // 2^51 / 4n, knn_mode_lim
     int n, force_fail;
 };
 template <typename TE, int KP, int KL>
@@ -1412,33 +1413,50 @@ __global__ __launch_bounds__(256) void k_merge_rank(
     const int nl = lpq * nsplit;
     // any value read is a valid bound (it only falls); floor: d^2 are integers
     const double qb = __longlong_as_double((long long)qthr[q]);
-    const double B = qb >= 4294967295.0 ? 4294967295.0 : floor(qb);
-
-    double d[KL];
+    const double B = qb >= 4294967294.0 ? 4294967294.0 : floor(qb);
+    const unsigned Bu = (unsigned)B;
+    // T: the smallest rejection bound of the merged lanes (and the state);
+    // read with the lists (one round of loads), reduced below
+    double T = KNN_INF, Td = KNN_INF;
+    if (lane < nsplit) T = part_T[(size_t)lane * nq_pad + q];
+    if (!first_step && lane == 63) {
+        T = fmin(T, st_T[2 * (size_t)q]);
+        Td = st_T[2 * (size_t)q + 1];
+    }
+    const int mode = fin ? knn_mode_lim<TE>(fa.meta, fa.n, fa.lim) : KNN_MODE_INT;
+    // list entries as 32-bit d^2 (exact integers < 2^31; +inf -> 0xffffffff,
+    // above every bound): half the registers of doubles, 5 -> 6 waves a SIMD
+    constexpr unsigned DINF = 0xffffffffu;
+    unsigned d[KL];
     int id[KL];
 #pragma unroll
     for (int e = 0; e < KL; e++) {
-        d[e] = KNN_INF;
+        d[e] = DINF;
         id[e] = 0;
     }
     int c = 0;
     if (lane < nl) {
-        const int s = lane / lpq, g = lane - s * lpq;
+        const int s = lpq == 2 ? lane >> 1 : lpq == 4 ? lane >> 2 : lane / lpq, g = lane - s * lpq;
         const size_t base = (((size_t)s * nq_pad + q) * lpq + g) * KL;
-        // the list is sorted: read it 4 entries at a time while the last
-        // one read is still at or below the bound (a late merge reads 1-2
-        // entries of most lists)
+        // the list is sorted: its first 4 entries, then the rest in one
+        // round if the 4th is still at or below the bound (two dependent
+        // rounds at most: the merge is latency-bound, one wave a query)
 #pragma unroll
-        for (int e0 = 0; e0 < KL; e0 += 4) {
-            if (e0 > 0 && !(d[e0 - 1] <= B)) break;
+        for (int e = 0; e < 4 && e < KL; e++) {
+            const double v = part_d[base + e];
+            d[e] = v < 4294967295.0 ? (unsigned)v : DINF;
+            id[e] = part_i[base + e];
+        }
+        if (KL > 4 && d[3] <= Bu) {
 #pragma unroll
-            for (int e = e0; e < e0 + 4 && e < KL; e++) {
-                d[e] = part_d[base + e];
+            for (int e = 4; e < KL; e++) {
+                const double v = part_d[base + e];
+                d[e] = v < 4294967295.0 ? (unsigned)v : DINF;
                 id[e] = part_i[base + e];
             }
         }
 #pragma unroll
-        for (int e = 0; e < KL; e++) c += d[e] <= B ? 1 : 0;   // a prefix (+inf past the end)
+        for (int e = 0; e < KL; e++) c += d[e] <= Bu ? 1 : 0;   // a prefix (+inf past the end)
     }
     double sdv = KNN_INF;
     int siv = -1, cs = 0;
@@ -1447,6 +1465,61 @@ __global__ __launch_bounds__(256) void k_merge_rank(
         siv = st_i[(size_t)q * KP + lane];
         cs = (siv >= 0 && sdv <= B) ? 1 : 0;
     }
+    // A tighter bound first: the (k+1)-th smallest key among the first HD
+    // entries of every list and the state entries.  It is at or above the
+    // (k+1)-th smallest key of all the entries (a subset's (k+1)-th is never
+    // below the whole set's), so the entries at or below it still hold the
+    // k + 1 smallest.  The shared bound B alone admitted ~100-170 entries a
+    // query at P = 1 (7 splits x 2 lists x 12), and the rank loop's
+    // broadcast LDS reads grow with C^2 / 64: 89 us a merge of 60000
+    // queries, nearly all of it those reads (rocprofv3, round 6).
+    unsigned long long lim = ~0ull;
+#ifndef KNN_MR_NOTIGHT
+    {
+        constexpr int HD = KL < 4 ? KL : 4;
+        const int hh = c < HD ? c : HD;    // lists are sorted: a prefix
+        const int chh = hh + cs;
+        int preh = 0, CH = 0;
+#pragma unroll
+        for (int b = 0; b < 5; b++) {
+            const unsigned long long m = __ballot((chh >> b) & 1);
+            preh += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << b;
+            CH += __popcll(m) << b;
+        }
+        if (CH > k) {
+#pragma unroll
+            for (int e = 0; e < HD; e++)
+                if (e < hh) buf[preh + e] = ((unsigned long long)d[e] << 32) | (unsigned)id[e];
+            if (cs) buf[preh + hh] = ((unsigned long long)(unsigned)sdv << 32) | (unsigned)siv;
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            unsigned long long bk = ~0ull;
+            for (int b0 = 0; b0 < CH; b0 += 64) {
+                const int my = b0 + lane;
+                const unsigned long long x = my < CH ? buf[my] : ~0ull;
+                int r = 0, j = 0;
+                for (; j + 4 <= CH; j += 4) {
+                    const knn_u64x2 u = *(const LDS_AS knn_u64x2 *)(buf + j);
+                    const knn_u64x2 w = *(const LDS_AS knn_u64x2 *)(buf + j + 2);
+                    r += (u.x < x ? 1 : 0) + (u.y < x ? 1 : 0) + (w.x < x ? 1 : 0) + (w.y < x ? 1 : 0);
+                }
+                for (; j < CH; j++) r += buf[j] < x ? 1 : 0;
+                const unsigned long long at = __ballot(my < CH && r == k);
+                if (at) bk = __shfl(x, __builtin_ctzll(at));
+            }
+            // keep the entries at or below it (the lists are sorted by d, so
+            // a prefix up to ties; counted and written entry by entry below)
+            lim = bk;
+            int c2 = 0;
+#pragma unroll
+            for (int e = 0; e < KL; e++)
+                c2 += (e < c && (((unsigned long long)d[e] << 32) | (unsigned)id[e]) <= bk) ? 1 : 0;
+            c = c2;
+            if (cs && (((unsigned long long)(unsigned)sdv << 32) | (unsigned)siv) > bk) cs = 0;
+            __builtin_amdgcn_wave_barrier();   // (the subset's slots are overwritten below)
+        }
+    }
+#endif
     // exclusive prefix of the per-lane counts (<= KL + 1 < 32): bit-sliced
     // through mbcnt
     const int ct = c + cs;
@@ -1457,21 +1530,19 @@ __global__ __launch_bounds__(256) void k_merge_rank(
         pre += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << b;
         C += __popcll(m) << b;
     }
+    {
+        int w = pre;
 #pragma unroll
-    for (int e = 0; e < KL; e++)
-        if (e < c) buf[pre + e] = ((unsigned long long)(unsigned)d[e] << 32) | (unsigned)id[e];
+        for (int e = 0; e < KL; e++) {
+            const unsigned long long key = ((unsigned long long)d[e] << 32) | (unsigned)id[e];
+            if (d[e] <= Bu && key <= lim) buf[w++] = key;
+        }
+    }
     if (cs) buf[pre + c] = ((unsigned long long)(unsigned)sdv << 32) | (unsigned)siv;
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
     const int kk = k + 1 < KP ? k + 1 : KP;   // entries the state keeps
-    // T: the smallest rejection bound of the merged lanes (and the state)
-    double T = KNN_INF, Td = KNN_INF;
-    if (lane < nsplit) T = part_T[(size_t)lane * nq_pad + q];
-    if (!first_step && lane == 63) {
-        T = fmin(T, st_T[2 * (size_t)q]);
-        Td = st_T[2 * (size_t)q + 1];
-    }
     for (int off = 32; off > 0; off >>= 1) {
         T = fmin(T, __shfl_xor(T, off));
         Td = fmin(Td, __shfl_xor(Td, off));
@@ -1479,9 +1550,7 @@ __global__ __launch_bounds__(256) void k_merge_rank(
     // fin: the records are written as the ranks come out; the query is
     // certified (or put on the rescan list, whose pass rewrites them) after
     const bool emit = fin != 0;
-    int mode = KNN_MODE_INT;
     if (fin) {
-        mode = knn_mode<TE>(fa.meta, fa.n);
         if (blockIdx.x == 0 && threadIdx.x == 0) *fa.mode_out = mode;
         // slots past the candidates: {inf, 0, 0}
         if (lane < k && lane >= C) {
@@ -1546,13 +1615,14 @@ __global__ __launch_bounds__(256) void k_merge_rank(
             // MNIST queries)
             int c2 = 0;
             if (lane < nl) {
-                const int s = lane / lpq, g = lane - s * lpq;
+                const int s = lpq == 2 ? lane >> 1 : lpq == 4 ? lane >> 2 : lane / lpq, g = lane - s * lpq;
                 const size_t base = (((size_t)s * nq_pad + q) * lpq + g) * KL;
 #pragma unroll
                 for (int e = 0; e < KL; e++) {
-                    d[e] = part_d[base + e];
+                    const double v = part_d[base + e];
+                    d[e] = v < 4294967295.0 ? (unsigned)v : DINF;
                     id[e] = part_i[base + e];
-                    c2 += d[e] < KNN_INF ? 1 : 0;   // a prefix
+                    c2 += d[e] != DINF ? 1 : 0;   // a prefix
                 }
             }
             const int cs2 = (!first_step && lane < KP && siv >= 0 && sdv < KNN_INF) ? 1 : 0;
@@ -1567,7 +1637,7 @@ __global__ __launch_bounds__(256) void k_merge_rank(
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int e = 0; e < KL; e++)
-                if (e < c2) buf[pre2 + e] = ((unsigned long long)(unsigned)d[e] << 32) | (unsigned)id[e];
+                if (e < c2) buf[pre2 + e] = ((unsigned long long)d[e] << 32) | (unsigned)id[e];
             if (cs2) buf[pre2 + c2] = ((unsigned long long)(unsigned)sdv << 32) | (unsigned)siv;
             __builtin_amdgcn_wave_barrier();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2548,6 +2618,7 @@ extern "C" int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const dou
     fa.fbound = fbound;
     fa.meta = meta;
     fa.n = n;
+    fa.lim = 2251799813685248.0 / (4.0 * (double)n);
     fa.force_fail = force_fail;
     const int fin = fin_out != nullptr;
     if (lpq < 1 || nsplit < 1 || lpq * nsplit > 64 || k <= 0 || k > kp || kp > 64 || nsplit > 64 ||
