@@ -22,13 +22,16 @@ from test_gpu_ring_rotation import loopback_dist
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("src", ["col-f64", "row-f64", "row-f32"])
+@pytest.mark.parametrize("src", ["col-f64", "col-f64-784", "row-f64", "row-f32"])
 def test_s8_block_equals_shadow8(knn, src):
+    """(col-f64-784: MNIST's row length, 13 column tiles of the column pack,
+    the last one half padding)"""
     import torch
     import mpiknn.ring as ring
     dt = "f32" if src.endswith("f32") else "f64"
     # fp32 INT mode needs n max^2 <= 2^23 (knn_i8_exact): 128 features
-    X = datasets.mnist_like(1000, 128 if dt == "f32" else 300, seed=3)[0]
+    shape = (2500, 784) if src.endswith("784") else (1000, 128 if dt == "f32" else 300)
+    X = datasets.mnist_like(*shape, seed=3)[0]
     X[5] = 0.0
     X[7] = 255.0
     m, n = X.shape
