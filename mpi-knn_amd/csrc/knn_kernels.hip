@@ -1375,12 +1375,14 @@ __global__ __launch_bounds__(256) void k_merge(
 // integer d^2 < 2^31, zeros never admitted) by ranking instead of argmin
 // rounds.  One wave per query.  The shared bound qthr[q] is an upper bound on
 // the query's (k+1)-th smallest d^2 over all rows (k + 1 distinct rows lie at
-// or below it), so no entry above it can be among the k + 1 smallest: every
-// list entry and state entry at or below it is compacted into LDS as a u64
-// key (d^2 << 32 | idx: u64 order is the reference's (d, idx) order, SURVEY
-// F1; keys are distinct), each candidate's rank is the number of smaller
-// keys, and rank r < k + 1 goes to state slot r.  The rank of a candidate
-// costs C compares a lane (C candidates, ~31..100 at the end of a search);
+// or below it), so no entry above it can be among the k + 1 smallest; the
+// (k+1)-th smallest key among the lists' first entries and the state is a
+// second such bound, usually far tighter.  Every list entry and state entry
+// at or below both is compacted into LDS as a u64 key (d^2 << 32 | idx: u64
+// order is the reference's (d, idx) order; keys are distinct),
+// each candidate's rank is the number of smaller keys, and rank r < k + 1
+// goes to state slot r.  The rank of a candidate costs C compares a lane
+// (C candidates, ~31..60 at the end of a search);
 // k_merge's k + 1 dependent wave-argmin rounds cost ~2k cycles each in
 // latency (rocprofv3: 33 us for 7500 queries, 0.19 ms for 60000).
 // State, T, Td and the publication as k_merge's INT mode (the (k+1)-th of
