@@ -1677,6 +1677,244 @@ __global__ __launch_bounds__(256) void k_merge_rank(
 }
 
 // ---------------------------------------------------------------------------
+// k_merge_rank16: k_merge_rank's fin pass without a state (the search's only
+// merge: a P = 1 search) when a query has at most 16 lists -- 16 lanes a
+// query, 4 queries a wave.  Same bounds, keys, ranks, records, certificate
+// and fallback as k_merge_rank (fin, first_step); a lane ranks the group's
+// candidates gl, gl + 16, ... against all of them.  k_merge_rank ran one
+// wave a query with 14 of 64 lanes holding lists: 651 VALU instructions a
+// query, most of them per-query work (loads, conversions, compaction, the
+// records' sqrt) done once a wave (SQ counters, round 6).
+// ---------------------------------------------------------------------------
+template <typename TE, int KL>
+__global__ __launch_bounds__(256) void k_merge_rank16(
+    const double *__restrict__ part_d, const int *__restrict__ part_i, const double *__restrict__ part_T,
+    int nsplit, int lpq, int nq, int nq_pad, int k, unsigned long long *__restrict__ qthr, knn_fin_args fa)
+{
+    constexpr int CAPG = 16 * KL + 4;   // a group's keys (+ pad: groups 32 bytes apart mod 256)
+    __shared__ __attribute__((aligned(16))) unsigned long long r16_buf[16 * CAPG];
+    constexpr unsigned DINF = 0xffffffffu;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int grp = lane >> 4, gl = lane & 15;
+    const int q = blockIdx.x * 16 + wave * 4 + grp;
+    const bool qv = q < nq;
+    if (__ballot(qv) == 0ull) return;   // wave-uniform; no workgroup barrier below
+    LDS_AS unsigned long long *buf = (LDS_AS unsigned long long *)r16_buf + (size_t)(wave * 4 + grp) * CAPG;
+    const unsigned long long gmask = 0xffffull << (16 * grp);
+    const unsigned long long ltmask = (1ull << lane) - 1ull;
+    const int nl = qv ? lpq * nsplit : 0;
+    const int qq = qv ? q : 0;
+    const double qb = __longlong_as_double((long long)qthr[qq]);
+    const double B = qb >= 4294967294.0 ? 4294967294.0 : floor(qb);
+    const unsigned Bu = (unsigned)B;
+    double T = KNN_INF;
+    if (qv && gl < nsplit) T = part_T[(size_t)gl * nq_pad + q];
+    const int mode = knn_mode_lim<TE>(fa.meta, fa.n, fa.lim);
+
+    unsigned d[KL];
+    int id[KL];
+#pragma unroll
+    for (int e = 0; e < KL; e++) {
+        d[e] = DINF;
+        id[e] = 0;
+    }
+    int c = 0;
+    if (gl < nl) {
+        const int sp = lpq == 2 ? gl >> 1 : lpq == 4 ? gl >> 2 : gl / lpq, g = gl - sp * lpq;
+        const size_t base = (((size_t)sp * nq_pad + q) * lpq + g) * KL;
+#pragma unroll
+        for (int e = 0; e < 4 && e < KL; e++) {
+            const double v = part_d[base + e];
+            d[e] = v < 4294967295.0 ? (unsigned)v : DINF;
+            id[e] = part_i[base + e];
+        }
+        if (KL > 4 && d[3] <= Bu) {
+#pragma unroll
+            for (int e = 4; e < KL; e++) {
+                const double v = part_d[base + e];
+                d[e] = v < 4294967295.0 ? (unsigned)v : DINF;
+                id[e] = part_i[base + e];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < KL; e++) c += d[e] <= Bu ? 1 : 0;   // a prefix
+    }
+    for (int off = 8; off > 0; off >>= 1) T = fmin(T, __shfl_xor(T, off));   // within the group
+
+    // the tighter bound: the (k+1)-th smallest key among the lists' first
+    // HD entries (k_merge_rank)
+    unsigned long long lim = ~0ull;
+    {
+        constexpr int HD = KL < 4 ? KL : 4;
+        const int hh = c < HD ? c : HD;
+        int preh = 0, CH = 0;
+#pragma unroll
+        for (int b = 0; b < 3; b++) {
+            const unsigned long long m = __ballot((hh >> b) & 1) & gmask;
+            preh += __popcll(m & ltmask) << b;
+            CH += __popcll(m) << b;
+        }
+#pragma unroll
+        for (int e = 0; e < HD; e++)
+            if (CH > k && e < hh) buf[preh + e] = ((unsigned long long)d[e] << 32) | (unsigned)id[e];
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (CH > k) {   // (group-uniform)
+            unsigned long long bk = ~0ull;
+            for (int b0 = 0; b0 < CH; b0 += 64) {
+                unsigned long long x[4];
+                int r[4];
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const int my = b0 + gl + 16 * t;
+                    x[t] = my < CH ? buf[my] : ~0ull;
+                    r[t] = 0;
+                }
+                int j = 0;
+                for (; j + 4 <= CH; j += 4) {
+                    const knn_u64x2 u = *(const LDS_AS knn_u64x2 *)(buf + j);
+                    const knn_u64x2 w = *(const LDS_AS knn_u64x2 *)(buf + j + 2);
+#pragma unroll
+                    for (int t = 0; t < 4; t++)
+                        r[t] += (u.x < x[t] ? 1 : 0) + (u.y < x[t] ? 1 : 0) + (w.x < x[t] ? 1 : 0) + (w.y < x[t] ? 1 : 0);
+                }
+                for (; j < CH; j++) {
+                    const unsigned long long u = buf[j];
+#pragma unroll
+                    for (int t = 0; t < 4; t++) r[t] += u < x[t] ? 1 : 0;
+                }
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const unsigned long long at = __ballot(b0 + gl + 16 * t < CH && r[t] == k) & gmask;
+                    if (at) bk = __shfl(x[t], __builtin_ctzll(at));
+                }
+            }
+            lim = bk;
+            int c2 = 0;
+#pragma unroll
+            for (int e = 0; e < KL; e++)
+                c2 += (e < c && (((unsigned long long)d[e] << 32) | (unsigned)id[e]) <= bk) ? 1 : 0;
+            c = c2;
+        }
+        __builtin_amdgcn_wave_barrier();   // (the subset's slots are overwritten below)
+    }
+    // compaction: the group's entries at or below both bounds
+    int pre = 0, C = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) {
+        const unsigned long long m = __ballot((c >> b) & 1) & gmask;
+        pre += __popcll(m & ltmask) << b;
+        C += __popcll(m) << b;
+    }
+    {
+        int w = pre;
+#pragma unroll
+        for (int e = 0; e < KL; e++) {
+            const unsigned long long key = ((unsigned long long)d[e] << 32) | (unsigned)id[e];
+            if (d[e] <= Bu && key <= lim) buf[w++] = key;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fa.mode_out = mode;
+    // slots past the candidates: {inf, 0, 0}
+    for (int p = gl; p < k; p += 16)
+        if (qv && p >= C) {
+            knn_neighbour_t rec;
+            rec.distance = KNN_INF;
+            rec.idx = 0;
+            rec.label = 0;
+            fa.out[(size_t)q * k + p] = rec;
+        }
+    double tau = KNN_INF, tk1 = KNN_INF;
+    for (int b0 = 0; b0 < C; b0 += 64) {   // (group-uniform trip count)
+        unsigned long long x[4];
+        int r[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int my = b0 + gl + 16 * t;
+            x[t] = my < C ? buf[my] : ~0ull;
+            r[t] = 0;
+        }
+        const int nt = (C - b0 + 15) >> 4;   // live slots a lane this round (group-uniform)
+        int j = 0;
+        for (; j + 4 <= C; j += 4) {
+            const knn_u64x2 u = *(const LDS_AS knn_u64x2 *)(buf + j);
+            const knn_u64x2 w = *(const LDS_AS knn_u64x2 *)(buf + j + 2);
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                if (t < nt)
+                    r[t] += (u.x < x[t] ? 1 : 0) + (u.y < x[t] ? 1 : 0) + (w.x < x[t] ? 1 : 0) + (w.y < x[t] ? 1 : 0);
+        }
+        for (; j < C; j++) {
+            const unsigned long long u = buf[j];
+#pragma unroll
+            for (int t = 0; t < 4; t++) r[t] += u < x[t] ? 1 : 0;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const bool live = b0 + gl + 16 * t < C;
+            if (live && r[t] < k) {
+                knn_neighbour_t rec;
+                rec.distance = sqrt((double)(unsigned)(x[t] >> 32));
+                rec.idx = (int)(unsigned)x[t] + 1;
+                rec.label = 0;
+                fa.out[(size_t)q * k + r[t]] = rec;
+            }
+            const unsigned long long a0 = __ballot(live && r[t] == k - 1) & gmask;
+            if (a0) tau = (double)(unsigned)(__shfl(x[t], __builtin_ctzll(a0)) >> 32);
+            const unsigned long long a1 = __ballot(live && r[t] == k) & gmask;
+            if (a1) tk1 = (double)(unsigned)(__shfl(x[t], __builtin_ctzll(a1)) >> 32);
+        }
+    }
+    const bool ok = mode == KNN_MODE_INT && !fa.force_fail && (T == KNN_INF || (C >= k && tau < T));
+    if (qv && !ok && C < k + 1 && mode == KNN_MODE_INT && !fa.force_fail) {
+        // fewer than k + 1 entries under the bounds: the k-th and (k+1)-th
+        // over every entry of the lists (k_merge_rank's fallback)
+        int c2 = 0;
+        if (gl < nl) {
+            const int sp = lpq == 2 ? gl >> 1 : lpq == 4 ? gl >> 2 : gl / lpq, g = gl - sp * lpq;
+            const size_t base = (((size_t)sp * nq_pad + q) * lpq + g) * KL;
+#pragma unroll
+            for (int e = 0; e < KL; e++) {
+                const double v = part_d[base + e];
+                d[e] = v < 4294967295.0 ? (unsigned)v : DINF;
+                id[e] = part_i[base + e];
+                c2 += d[e] != DINF ? 1 : 0;   // a prefix
+            }
+        }
+        int pre2 = 0, C2 = 0;
+#pragma unroll
+        for (int b = 0; b < 5; b++) {
+            const unsigned long long m = __ballot((c2 >> b) & 1) & gmask;
+            pre2 += __popcll(m & ltmask) << b;
+            C2 += __popcll(m) << b;
+        }
+#pragma unroll
+        for (int e = 0; e < KL; e++)
+            if (e < c2) buf[pre2 + e] = ((unsigned long long)d[e] << 32) | (unsigned)id[e];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int my0 = 0; my0 < C2; my0 += 16) {
+            const int my = my0 + gl;
+            const unsigned long long x = my < C2 ? buf[my] : ~0ull;
+            int r = 0;
+            for (int j = 0; j < C2; j++) r += buf[j] < x ? 1 : 0;
+            const unsigned long long a0 = __ballot(my < C2 && r == k - 1) & gmask;
+            if (a0) tau = (double)(unsigned)(__shfl(x, __builtin_ctzll(a0)) >> 32);
+            const unsigned long long a1 = __ballot(my < C2 && r == k) & gmask;
+            if (a1) tk1 = (double)(unsigned)(__shfl(x, __builtin_ctzll(a1)) >> 32);
+        }
+    }
+    if (qv && !ok && gl == 0) {
+        fa.fail_list[atomicAdd(fa.fail_count, 1)] = q;
+        fa.fbound[q] = (fa.force_fail || mode != KNN_MODE_INT) ? KNN_INF : sqrt(tau);
+        if (mode == KNN_MODE_INT && !fa.force_fail)
+            qthr[q] = (unsigned long long)__double_as_longlong(sizeof(TE) == 4 ? (double)__double2float_ru(tk1) : tk1);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_finalize: one wave per query.  Order by (sqrt(S), idx) -- the key the
 // reference keeps (knn-serial.c:86-90) -- drop S == 0, and certify: every
 // candidate outside the state has approx d^2 >= T, hence exact S >= T - E
@@ -2626,6 +2864,22 @@ extern "C" int knn_launch_merge_rank(int dtype, int kp, int kl, int k, const dou
     if (lpq < 1 || nsplit < 1 || lpq * nsplit > 64 || k <= 0 || k > kp || kp > 64 || nsplit > 64 ||
         (kl != KNN_I8_KL_S && kl != KNN_I8_KL))
         return KNN_ERR_INVALID;
+#ifndef KNN_NO_RANK16
+    if (fin && first_step && lpq * nsplit <= 16) {
+        // the search's only merge (P = 1): 16 lanes a query
+        const dim3 g16((unsigned)((nq + 15) / 16));
+        hipStream_t s16 = (hipStream_t)stream;
+#define RANK16(T, KL)                                                                              \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_merge_rank16<T, KL>), g16, dim3(256), 0, s16, part_d, part_i, \
+                           part_T, nsplit, lpq, nq, nq_pad, k, (unsigned long long *)qthr, fa)
+        if (dtype == KNN_F64 && kl == KNN_I8_KL_S) RANK16(double, KNN_I8_KL_S);
+        else if (dtype == KNN_F64) RANK16(double, KNN_I8_KL);
+        else if (kl == KNN_I8_KL_S) RANK16(float, KNN_I8_KL_S);
+        else RANK16(float, KNN_I8_KL);
+#undef RANK16
+        return hip_status();
+    }
+#endif
     const int cap = (lpq * nsplit * kl + kp + 1) & ~1;   // every candidate; 16-byte rows
     const size_t lds = 4 * (size_t)cap * sizeof(unsigned long long);
     const dim3 grid((unsigned)((nq + 3) / 4));
