@@ -460,7 +460,8 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
         # HIP events on the merge's stream, the engine's algorithmic byte
         # count) and the pack / norm pass (torch events on its stream)
         "merge": {
-            "kernel": "k_merge_rank" if cbits == 8 else "k_merge",
+            # (a P = 1 int8 search's only merge runs as k_merge_rank16)
+            "kernel": ("k_merge_rank16" if P == 1 else "k_merge_rank") if cbits == 8 else "k_merge",
             "bound": "hbm",
             "ms_per_step": mk_ms / max(prof_steps, 1),
             "launches_per_step": mk_n / max(prof_steps, 1),
