@@ -390,8 +390,7 @@ def run_workload(workload, steps, warmup, args, torch, dist, rank, P, local, nch
     # the MFMA the contraction ran on: fp32 searches on exactly representable
     # 8-bit-style integer data contract on fp16 MFMA (include/knn.h)
     split = engine.ctx.split()
-    kernel = "k_dist_topk_i8" if cbits == 8 else ("k_dist_split" if split and
-                                                  os.environ.get("KNN_SPLIT_V1", "0") != "1" else "k_dist_topk")
+    kernel = "k_dist_topk_i8" if cbits == 8 else ("k_dist_split" if split else "k_dist_topk")
     traffic, traffic_src, traffic_stale = None, None, None
     try:
         with open(args.traffic_json) as f:
