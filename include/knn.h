@@ -28,20 +28,12 @@
  *                         contraction in line runs)
  *   KNN_I8_KL=17          17-entry int8 lane lists instead of 12
  *   KNN_SPLITS=s          corpus splits per launch instead of the model's
- *   KNN_NO_FUSE=1         fold received byte blocks one launch each
- *   KNN_NO_PAIR_FUSED=1   the own block's step keeps a merge of its own
- *                         instead of sharing the fused step's
- *   KNN_NO_QSUM=1         int8 kernels without the cross-split summaries
- *   KNN_I8_W8=1           12-entry int8 lists on the 8-wave kernel (128-row
- *                         tiles) instead of the 64-row half-tile kernel
  *   KNN_ORDER=1 / KNN_NO_ORDER=1
  *                         GEMM-mode merge in the clustered query order
  *                         (default past 64 MB blocks) / always index order
  *   KNN_I8_QG1=1          one query group a wave on rows of <= 128 bytes
  *                         (the half-tile kernel otherwise carries two: 256
  *                         queries a workgroup sharing each staged row)
- *   KNN_NO_RANK_MERGE=1   int8 lists merged by k_merge's argmin rounds
- *                         instead of k_merge_rank
  *   KNN_FORCE_RESCAN=1    send every query through the exact rescan pass
  *   KNN_NO_RESEARCH8=1    no int8 re-search (65-entry lists) of uncertified
  *                         queries of a single-block search before the rescan
@@ -62,6 +54,8 @@
  *                         group's timeout)
  *   KNN_RING_LOOPBACK=1   P virtual ranks on device 0 (tests)
  *   KNN_NO_SHADOW_RING=1  ring moves element blocks, not shadow/byte blocks
+ *   KNN_XCD_ORDER=1       distance launches in the XCD-grouped workgroup
+ *                         order instead of split-major
  *   KNN_MAT / KNN_MPI_COMPAT  the CLIs: .mat path, bug-compatible mode
  *   (mpiknn/ring.py: KNN_NO_S8=1 packs element blocks, not the byte block
  *   of knn_block_pack_s8)
@@ -345,15 +339,14 @@ KNN_API int knn_ctx_step(knn_ctx_t *ctx, const void *d_cblock, size_t nc,
  * once).  Byte blocks (knn_ctx_shadow == 2) share one distance launch per 8
  * blocks, which counts as ONE step of the lag rule above: none of the
  * blocks may be overwritten before KNN_STEP_LAG further steps (or
- * knn_ctx_end).  fp16 shadow blocks fold one block a step (and so do
- * byte blocks with KNN_NO_FUSE=1). */
+ * knn_ctx_end).  fp16 shadow blocks fold one block a step. */
 KNN_API int knn_ctx_step_shadow_n(knn_ctx_t *ctx, int nblk, const void *const *d_sblocks,
                                   const size_t *nc, const size_t *c_base, void *stream);
 /* The same for nblk resident element blocks (d_cblocks[b]: packed blocks of
  * capacity block_cap): a search on the split-fp16 filter (real-valued data,
  * knn_ctx_split) folds up to 8 of them in one distance launch and one merge,
  * which count as ONE step of the lag rule; other searches fold one block a
- * step (KNN_NO_FUSE=1 too). */
+ * step. */
 KNN_API int knn_ctx_step_n(knn_ctx_t *ctx, int nblk, const void *const *d_cblocks, const size_t *nc,
                            const size_t *c_base, void *stream);
 

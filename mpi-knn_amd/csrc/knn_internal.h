@@ -112,7 +112,7 @@ typedef struct {
 static inline int knn_i8_kl(int kp) { return kp <= KNN_KP_M ? KNN_I8_KL_S : KNN_I8_KL_L; }
 /* lists per query: 2 for the 65-entry lists (k > 32) and for the 12-entry
  * lists on 64-row half tiles (the k <= 32 default); 4 for the 8-wave
- * kernel on 128-row tiles (17-entry lists, or KNN_I8_W8=1) */
+ * kernel on 128-row tiles (17-entry lists) */
 static inline int knn_i8_lpq(int kp, int kl) { return kp <= KNN_KP_M && kl != KNN_I8_KL_S ? 4 : 2; }
 /* query groups a wave of the int8 kernel: 2 for the half-tile kernel on
  * rows of <= 4 K-steps (SIFT's n = 128: a workgroup of 256 queries, A
