@@ -32,7 +32,7 @@ def mnist_real(m=60000, n=784, seed=1234, noise_seed=0x5EA1):
     """The real-valued MNIST variant (mnist_train_svd.mat is
     real-valued): mnist_like(m, n, seed) / 255 + N(0, 1e-3) (numpy
     default_rng(noise_seed)), fp64.  Not integer, so the engine runs its
-    GEMM mode: fp64 MFMA filter + exact reference-order re-rank."""
+    GEMM mode: the split-fp16 filter + exact reference-order re-rank."""
     X, y = mnist_like(m, n, seed)
     X /= 255.0
     X += np.random.default_rng(noise_seed).normal(0, 1e-3, X.shape)
