@@ -302,9 +302,9 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 s_coff = 0;
                 if (++s_t == s_t1) {   // next block of the launch
                     s_b++;
-                    s_row = (const signed char *)(uintptr_t)i8_rfl64((long long)tab->ptr[s_b]);
-                    s_nrow = (const int *)(uintptr_t)i8_rfl64((long long)tab->nptr[s_b]);
-                    s_t1 = i8_rfl(tab->t0[s_b + 1]);
+                    s_row = (const signed char *)(uintptr_t)i8_tab64(&tab->ptr[s_b]);
+                    s_nrow = (const int *)(uintptr_t)i8_tab64(&tab->nptr[s_b]);
+                    s_t1 = i8_tab32(&tab->t0[s_b + 1]);
                 } else {
                     s_row += (size_t)TR * rs;
                     s_nrow += TR;
@@ -611,13 +611,22 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     };
 
     // ---- main loop -------------------------------------------------------------
+    // PF2 (half-tile kernel, long rows): A fragments are read two K-steps
+    // ahead instead of one, so a read has four MFMAs (two of this wave's
+    // K-steps) to land under instead of two.  Barrier B(y) then sits two
+    // K-steps before chunk y's first one; every read of chunk y - 1 was
+    // issued before it, and the lgkmcnt(0) ahead of the barrier has seen
+    // them complete, so the stage issued after B(y) may overwrite chunk y -
+    // 1's slot (as with one-deep reads, whose B(y) sits a K-step later).
+    constexpr bool PF2 = TM == 2 && QG == 1 && NKS >= 8 && NKS <= 25;   // (28 K-steps spill)
     if (total > 0) {
 #pragma unroll
         for (int y = 0; y < NST - 2; y++) stage();
         wait_next();
         __builtin_amdgcn_s_barrier();
-        knn_v4i acur[MB], anxt[MB];
+        knn_v4i acur[MB], anxt[MB], anx2[MB];
         rdA(0, 0, acur);
+        if constexpr (PF2) rdA(0, 1, anxt);
         stage();
         int x = 0;
         e_b = i8_blk_of(tab, t_lo);
@@ -629,9 +638,9 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             if (t == e_t1) {   // the epilogue's block moves on
                 e_b++;
                 e_t0 = e_t1;
-                e_t1 = i8_rfl(tab->t0[e_b + 1]);
-                c_base = (long)i8_rfl64(tab->base[e_b]);
-                nc = i8_rfl(tab->nc[e_b]);
+                e_t1 = i8_tab32(&tab->t0[e_b + 1]);
+                c_base = (long)i8_tab64(&tab->base[e_b]);
+                nc = i8_tab32(&tab->nc[e_b]);
             }
             // the tile's accumulators start at its init words (read at the
             // tile's start, straight into the accumulator registers: held
@@ -645,6 +654,51 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 for (int bb = 0; bb < MB; bb++)
 #pragma unroll
                     for (int i = 0; i < 16; i++) acc[0][bb][i] = 0;
+            }
+            if constexpr (PF2) {
+                // flat K-steps f of the tile; the fragments of f + 2 are read
+                // at f (the next tile's first two K-steps at f = NKS - 2,
+                // NKS - 1), behind B(y) when f + 2 opens chunk y
+                const int x0 = x;
+                const bool more = x0 + NCH < total;   // a next tile
+#pragma unroll
+                for (int f = 0; f < NKS; f++) {
+                    const int fn = f + 2;
+                    if (fn < NKS) {
+                        if ((fn & 3) == 0) {
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            wait_next();
+                            __builtin_amdgcn_s_barrier();   // B(x0 + fn / 4)
+                            rdA(x0 + (fn >> 2), 0, anx2);
+                            stage();
+                        } else {
+                            rdA(x0 + (fn >> 2), fn & 3, anx2);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    } else if (more) {
+                        if (fn == NKS) {
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            wait_next();
+                            __builtin_amdgcn_s_barrier();   // B(x0 + NCH)
+                            rdA(x0 + NCH, 0, anx2);
+                            stage();
+                        } else {
+                            rdA(x0 + NCH, 1, anx2);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    }
+#pragma unroll
+                    for (int bb = 0; bb < MB; bb++)
+                        acc[0][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(acur[bb], qf[0][f], acc[0][bb], 0, 0, 0);
+#pragma unroll
+                    for (int bb = 0; bb < MB; bb++) {
+                        acur[bb] = anxt[bb];
+                        anxt[bb] = anx2[bb];
+                    }
+                }
+                x = x0 + NCH;
+                epilogue(t, acc, x);
+                continue;
             }
 #pragma unroll
             for (int c = 0; c < NCH; c++) {

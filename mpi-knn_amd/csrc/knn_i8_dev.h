@@ -144,6 +144,23 @@ __device__ __forceinline__ long long i8_rfl64(long long v)
     return (long long)(((unsigned long long)hi << 32) | lo);
 }
 // block of global tile t (t inside the launch's tiles)
+// Block-table words of a taken block switch (the staging cursor's and the
+// epilogue's): read through asm, so the compiler cannot hoist them out of
+// the rarely taken branch.  Hoisted, the reads ran at every stage, and the
+// lgkmcnt(0) their readfirstlane needs drained the A-fragment reads issued
+// just before them.
+__device__ __forceinline__ long long i8_tab64(const LDS_AS void *p)
+{
+    long long v;
+    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(size_t)p) : "memory");
+    return i8_rfl64(v);
+}
+__device__ __forceinline__ int i8_tab32(const LDS_AS void *p)
+{
+    int v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(size_t)p) : "memory");
+    return i8_rfl(v);
+}
 __device__ __forceinline__ int i8_blk_of(const LDS_AS i8_tab_lds *tab, int t)
 {
     int b = 0;
