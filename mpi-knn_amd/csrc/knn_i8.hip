@@ -312,6 +312,42 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             }
         }
     };
+    // PF2's staging (the two-deep loop below): the chunk staged behind B(y)
+    // is z = y + NST - 2, and y's position in its tile is static at every
+    // call site, so z's position pz is too.  The chunk offset then rides in
+    // soffset against one descriptor of the tile's rows (cached: rebuilt once
+    // a tile), the norm piece goes out only at the site of a tile's first
+    // chunk and the cursor advances only at the site of its last -- where
+    // stage() spent ~40 scalar instructions a chunk on offsets, compares and
+    // an exec-masked branch.  Past the split's end the last tile's rows are
+    // re-staged (their slots are never read: the static count of pieces is
+    // what the ring's waits assume).
+    knn_v4i s_rs = i8_rsrc(s_row);
+    auto stage_at = [&](int pz) {
+        const unsigned dst = lds0 + ((unsigned)s_x % NST) * (unsigned)CHB + (unsigned)wave_s * (unsigned)(CHB / W);
+        bglds16x2s(s_rs, voff[0], voff[1], 128u * (unsigned)pz, dst);
+        // (unconditional: past the split's end the cursor stays on the last
+        // tile, so this re-stages that tile's words into its own slot --
+        // identical bytes; a uniform branch here cost 242 VGPRs of spills)
+        if (pz == 0)
+            bglds16m(i8_rsrc(s_nrow + WPW * wave_s),
+                     lane < WPW / 4 ? 16u * lane : 4u * (unsigned)c_rows_pad + 16u * (lane - WPW / 4),
+                     lds0 + NORM0 + ((unsigned)s_t % NST) * (unsigned)NRB + (unsigned)NSEG * wave_s,
+                     (1ull << (WPW / 2)) - 1);
+        s_x++;
+        if (pz == NCH - 1 && s_x < total) {   // the next tile
+            if (++s_t == s_t1) {   // next block of the launch
+                s_b++;
+                s_row = (const signed char *)(uintptr_t)i8_tab64(&tab->ptr[s_b]);
+                s_nrow = (const int *)(uintptr_t)i8_tab64(&tab->nptr[s_b]);
+                s_t1 = i8_tab32(&tab->t0[s_b + 1]);
+            } else {
+                s_row += (size_t)TR * rs;
+                s_nrow += TR;
+            }
+            s_rs = i8_rsrc(s_row);
+        }
+    };
     // the next chunk's own pieces landed: the NST - 3 chunks staged after it
     // may stay in flight.  One-chunk tiles (SIFT) count each stage's norm
     // piece too: counted as PW a stage, the wait also drained a third of the
@@ -628,6 +664,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         rdA(0, 0, acur);
         if constexpr (PF2) rdA(0, 1, anxt);
         stage();
+        if constexpr (PF2) s_rs = i8_rsrc(s_row);   // the prologue's stages moved the cursor
         int x = 0;
         e_b = i8_blk_of(tab, t_lo);
         e_t0 = i8_rfl(tab->t0[e_b]);
@@ -658,9 +695,14 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             if constexpr (PF2) {
                 // flat K-steps f of the tile; the fragments of f + 2 are read
                 // at f (the next tile's first two K-steps at f = NKS - 2,
-                // NKS - 1), behind B(y) when f + 2 opens chunk y
+                // NKS - 1), behind B(y) when f + 2 opens chunk y.  The last
+                // tile does the same (every wave of the workgroup runs the
+                // same tiles, so the extra barrier matches; the chunk it
+                // opens is a tail re-stage, read and never used): a runtime
+                // "next tile?" branch here made the compiler copy the
+                // fragment registers through waits at every tile's end
                 const int x0 = x;
-                const bool more = x0 + NCH < total;   // a next tile
+                constexpr bool more = true;
 #pragma unroll
                 for (int f = 0; f < NKS; f++) {
                     const int fn = f + 2;
@@ -670,7 +712,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x0 + fn / 4)
                             rdA(x0 + (fn >> 2), 0, anx2);
-                            stage();
+                            stage_at(((fn >> 2) + NST - 2) % NCH);
                         } else {
                             rdA(x0 + (fn >> 2), fn & 3, anx2);
                             __builtin_amdgcn_sched_barrier(0);
@@ -681,7 +723,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x0 + NCH)
                             rdA(x0 + NCH, 0, anx2);
-                            stage();
+                            stage_at((NST - 2) % NCH);
                         } else {
                             rdA(x0 + NCH, 1, anx2);
                             __builtin_amdgcn_sched_barrier(0);

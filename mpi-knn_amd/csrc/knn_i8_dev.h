@@ -115,6 +115,39 @@ __device__ __forceinline__ void bglds16x2(knn_v4i rsrc, unsigned v0, unsigned v1
                  : "memory", "scc");
 }
 
+// the same two pieces at byte offset soff (soffset: a chunk's offset inside
+// its tile rows, so one descriptor serves the tile)
+__device__ __forceinline__ void bglds16x2s(knn_v4i rsrc, unsigned v0, unsigned v1, unsigned soff, unsigned lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %1, %5 offen lds\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %3, %1, %5 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "s"(rsrc), "v"(v0), "v"(v1), "s"(__builtin_amdgcn_readfirstlane(lds_dst)),
+                   "s"(__builtin_amdgcn_readfirstlane(soff))
+                 : "memory", "scc");
+}
+
+// one piece from the lanes of `lanes` only (exec set and restored inside
+// the asm: no divergent region for the compiler to structure around the
+// loop's live registers -- as a C++ branch at PF2's static norm-piece site it
+// pushed the 25-K-step kernel into 242 VGPRs of spills)
+__device__ __forceinline__ void bglds16m(knn_v4i rsrc, unsigned voff, unsigned lds_dst, unsigned long long lanes)
+{
+    unsigned keep;
+    unsigned long long ex;
+    asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %5\n\t"
+                 "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0\n\t"
+                 "s_mov_b64 exec, %1"
+                 : "=&s"(keep), "=&s"(ex)
+                 : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst)), "s"(lanes)
+                 : "memory");
+}
+
 // buffer descriptor of a wave-uniform base, pinned to SGPRs (the base comes
 // from the LDS block table through readfirstlane; under register pressure
 // the allocator otherwise left the descriptor in VGPRs)
