@@ -140,7 +140,11 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     constexpr int WPW = TR / W;             // norm words a wave stages of each array
     constexpr int NSEG = 8 * WPW;           // a wave's staged piece (both arrays)
     constexpr int NORM0 = NST * CHB;        // norm ring: [NST][W][slot words, init words]
-    constexpr int BUF0 = NORM0 + NST * NRB; // [W][QG][NB][64] survivor d^2, then ids
+    // norm ring: NNR >= NST tile slots; a one-tile chunk ring (NST = chunks
+    // a tile, e.g. 7) takes 8, a power of two, so that no epilogue or norm
+    // stage computes a modulo-7
+    constexpr int NNR = NST == (NKS + 3) / 4 ? 8 : NST;
+    constexpr int BUF0 = NORM0 + NNR * NRB; // [W][QG][NB][64] survivor d^2, then ids
     constexpr int XB0 = BUF0 + 2 * W * QG * NB * 256;   // RHN = 2: [8][32] bound exchange (u4, v8, v16)
     constexpr int TB0 = XB0 + (RHN == 2 ? 3 * 8 * 32 * 4 : 0);   // block table
     static_assert(MB == 2 || MB == 4, "m-blocks a wave");
@@ -293,7 +297,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             if (lane < WPW / 2)
                 bglds16(i8_rsrc(s_nrow + WPW * wave_s),
                         lane < WPW / 4 ? 16u * lane : 4u * (unsigned)c_rows_pad + 16u * (lane - WPW / 4),
-                        lds0 + NORM0 + ((unsigned)s_t % NST) * (unsigned)NRB + (unsigned)NSEG * wave_s);
+                        lds0 + NORM0 + ((unsigned)s_t % NNR) * (unsigned)NRB + (unsigned)NSEG * wave_s);
         }
         s_x++;
         if (s_x < total) {
@@ -323,8 +327,14 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // re-staged (their slots are never read: the static count of pieces is
     // what the ring's waits assume).
     knn_v4i s_rs = i8_rsrc(s_row);
+    // With a one-tile ring (NST == NCH) the slot of a chunk is its position
+    // in its tile: static, like pz, so neither the stage's LDS address nor
+    // the fragment reads' need slot arithmetic (rdA's base folds into the
+    // ds_read offset)
+    constexpr bool SSLOT = NST == NCH;
     auto stage_at = [&](int pz) {
-        const unsigned dst = lds0 + ((unsigned)s_x % NST) * (unsigned)CHB + (unsigned)wave_s * (unsigned)(CHB / W);
+        const unsigned dst = lds0 + (SSLOT ? (unsigned)pz : (unsigned)s_x % NST) * (unsigned)CHB +
+                             (unsigned)wave_s * (unsigned)(CHB / W);
         bglds16x2s(s_rs, voff[0], voff[1], 128u * (unsigned)pz, dst);
         // (unconditional: past the split's end the cursor stays on the last
         // tile, so this re-stages that tile's words into its own slot --
@@ -332,7 +342,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         if (pz == 0)
             bglds16m(i8_rsrc(s_nrow + WPW * wave_s),
                      lane < WPW / 4 ? 16u * lane : 4u * (unsigned)c_rows_pad + 16u * (lane - WPW / 4),
-                     lds0 + NORM0 + ((unsigned)s_t % NST) * (unsigned)NRB + (unsigned)NSEG * wave_s,
+                     lds0 + NORM0 + ((unsigned)s_t % NNR) * (unsigned)NRB + (unsigned)NSEG * wave_s,
                      (1ull << (WPW / 2)) - 1);
         s_x++;
         if (pz == NCH - 1 && s_x < total) {   // the next tile
@@ -363,7 +373,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // accumulator init words of tile tt for the wave's MB m-blocks (the C
     // operand of the tile's first K-step): 4 ds_read_b128 an m-block
     auto rdI = [&](int tt, knn_v16i (&ini)[MB]) {
-        const LDS_AS char *p = (const LDS_AS char *)smem + NORM0 + ((unsigned)tt % NST) * NRB + NSEG / 2;
+        const LDS_AS char *p = (const LDS_AS char *)smem + NORM0 + ((unsigned)tt % NNR) * NRB + NSEG / 2;
 #pragma unroll
         for (int bb = 0; bb < MB; bb++) {
             knn_v4i r[4];
@@ -405,7 +415,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // their L[S8] / L[S16])
     constexpr bool REREAD = KL != KNN_I8_KL_L;
     // (QG = 2: no summaries -- their 8 VGPRs a group spill there)
-    constexpr bool SUM = REREAD && KL == KNN_I8_KL_S && QG == 1;
+    // (the two-deep-prefetch kernels below (PF2): none either -- they
+    // measured as worth nothing at P = 1 and at the P = 8 fused shape
+    // (DESIGN.md sec.8), and their pointer and 8 VGPRs spilled there, with a
+    // vmcnt(0) reload draining the staging ring every second tile)
+    constexpr bool PF2 = TM == 2 && QG == 1 && NKS >= 8 && NKS <= 25;
+    constexpr bool SUM = REREAD && KL == KNN_I8_KL_S && QG == 1 && !PF2;
     constexpr int S8 = 8 / LPQ - 1, S16 = 16 / LPQ - 1;
     int q_pubx[QG];
 #pragma unroll
@@ -570,7 +585,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     constexpr bool ACCF = SHORT;
     auto epilogue = [&](int t, knn_v16i (&A)[QG][MB], int xdone) {
         const int lt = t - e_t0;
-        const LDS_AS char *cn = (const LDS_AS char *)smem + NORM0 + ((unsigned)t % NST) * NRB;
+        const LDS_AS char *cn = (const LDS_AS char *)smem + NORM0 + ((unsigned)t % NNR) * NRB;
         const int row0 = lt * TR + 32 * MB * rh;
         const long gt0 = (long)c_base + row0;
         const bool rmask = row0 + 32 * MB > nc;
@@ -654,7 +669,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // issued before it, and the lgkmcnt(0) ahead of the barrier has seen
     // them complete, so the stage issued after B(y) may overwrite chunk y -
     // 1's slot (as with one-deep reads, whose B(y) sits a K-step later).
-    constexpr bool PF2 = TM == 2 && QG == 1 && NKS >= 8 && NKS <= 25;   // (28 K-steps spill)
+    // (PF2 is defined with the bounds above: 28 K-steps spill)
     if (total > 0) {
 #pragma unroll
         for (int y = 0; y < NST - 2; y++) stage();
@@ -711,10 +726,10 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x0 + fn / 4)
-                            rdA(x0 + (fn >> 2), 0, anx2);
+                            rdA(SSLOT ? (fn >> 2) : x0 + (fn >> 2), 0, anx2);
                             stage_at(((fn >> 2) + NST - 2) % NCH);
                         } else {
-                            rdA(x0 + (fn >> 2), fn & 3, anx2);
+                            rdA(SSLOT ? (fn >> 2) : x0 + (fn >> 2), fn & 3, anx2);
                             __builtin_amdgcn_sched_barrier(0);
                         }
                     } else if (more) {
@@ -722,13 +737,17 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x0 + NCH)
-                            rdA(x0 + NCH, 0, anx2);
+                            rdA(SSLOT ? 0 : x0 + NCH, 0, anx2);
                             stage_at((NST - 2) % NCH);
                         } else {
-                            rdA(x0 + NCH, 1, anx2);
+                            rdA(SSLOT ? 0 : x0 + NCH, 1, anx2);
                             __builtin_amdgcn_sched_barrier(0);
                         }
                     }
+                    // one lgkmcnt wait for the K-step's fragments (the
+                    // compiler waits before the asm that "defines" them)
+                    // instead of one before each MFMA
+                    asm volatile("" : "+v"(acur[0]), "+v"(acur[1]));
 #pragma unroll
                     for (int bb = 0; bb < MB; bb++)
                         acc[0][bb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(acur[bb], qf[0][f], acc[0][bb], 0, 0, 0);
@@ -1010,7 +1029,7 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int lpq, int k, const void *qs
         else if (nks <= 4) launch_i8<KNN_I8_KL_S, 4, 4, 2, 8, 5, 2>(I8_ARGS);
         else if (nks <= 8) launch_i8<KNN_I8_KL_S, 8, 4, 2, 8, 5, 2>(I8_ARGS);
         else if (nks <= 16) launch_i8<KNN_I8_KL_S, 16, 4, 2, 8, 5, 2>(I8_ARGS);
-        else if (nks <= 25) launch_i8<KNN_I8_KL_S, 25, 4, 2, 8, 5, 2>(I8_ARGS);
+        else if (nks <= 25) launch_i8<KNN_I8_KL_S, 25, 4, 2, 7, 5, 2>(I8_ARGS);   // one-tile ring (SSLOT)
         else launch_i8<KNN_I8_KL_S, 28, 4, 2, 8, 5, 2>(I8_ARGS);
     } else if (kl == KNN_I8_KL_S) {
         // 12-entry lists merge cheaply: 5-entry buffers (merging sooner)
