@@ -358,6 +358,38 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
             s_rs = i8_rsrc(s_row);
         }
     };
+    // One-chunk tiles (SIFT's <= 4 K-steps; PW = 2): every stage opens a
+    // tile, so stage1 keeps the ring slot and the norm-ring slot as counters
+    // (NST = 7 there: no modulo-7 a stage), the chunk at soffset 0 of the
+    // tile's cached descriptor, the norm piece under an asm exec mask (the
+    // tail re-stages the last tile's words, as stage() does for these tiles)
+    // and the cursor one tile on -- stage()'s offset arithmetic and branches
+    // ran once a tile of 16 MFMAs here.  s_slot / s_nslot / s_rs are set
+    // from the cursor after the prologue's stages.
+    constexpr bool ONE = NCH == 1 && PW == 2;
+    int s_slot = 0, s_nslot = 0;
+    auto stage1 = [&]() {
+        const unsigned dst = lds0 + (unsigned)s_slot * (unsigned)CHB + (unsigned)wave_s * (unsigned)(CHB / W);
+        bglds16x2s(s_rs, voff[0], voff[1], 0u, dst);
+        bglds16m(i8_rsrc(s_nrow + WPW * wave_s),
+                 lane < WPW / 4 ? 16u * lane : 4u * (unsigned)c_rows_pad + 16u * (lane - WPW / 4),
+                 lds0 + NORM0 + (unsigned)s_nslot * (unsigned)NRB + (unsigned)NSEG * wave_s, (1ull << (WPW / 2)) - 1);
+        s_x++;
+        s_slot = s_slot == NST - 1 ? 0 : s_slot + 1;
+        if (s_x < total) {
+            if (++s_t == s_t1) {   // next block of the launch
+                s_b++;
+                s_row = (const signed char *)(uintptr_t)i8_tab64(&tab->ptr[s_b]);
+                s_nrow = (const int *)(uintptr_t)i8_tab64(&tab->nptr[s_b]);
+                s_t1 = i8_tab32(&tab->t0[s_b + 1]);
+            } else {
+                s_row += (size_t)TR * rs;
+                s_nrow += TR;
+            }
+            s_rs = i8_rsrc(s_row);
+            s_nslot = s_nslot == NNR - 1 ? 0 : s_nslot + 1;
+        }
+    };
     // the next chunk's own pieces landed: the NST - 3 chunks staged after it
     // may stay in flight.  One-chunk tiles (SIFT) count each stage's norm
     // piece too: counted as PW a stage, the wait also drained a third of the
@@ -587,9 +619,11 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         const int lt = t - e_t0;
         const LDS_AS char *cn = (const LDS_AS char *)smem + NORM0 + ((unsigned)t % NNR) * NRB;
         const int row0 = lt * TR + 32 * MB * rh;
-        const long gt0 = (long)c_base + row0;
         const bool rmask = row0 + 32 * MB > nc;
-        const int idb = (int)(c_base + row0) + 4 * h;
+        // (32-bit row ids: every id is an int, so the low words' difference
+        // is the difference; the 64-bit compares ran as VALU ops a tile)
+        const int gt0 = (int)c_base + row0;
+        const int idb = gt0 + 4 * h;
         if constexpr (REREAD) {
             if (qthr != nullptr) {
                 if (q_ready >= 0 && xdone > q_ready) qthr_apply();
@@ -598,8 +632,9 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         }
 #pragma unroll
         for (int g = 0; g < QG; g++) {
-        const long gw0 = (long)q_base + qrow0 + 128 * g + 32 * qg;
-        const bool masked = rmask || (gw0 < gt0 + 32 * MB && gt0 < gw0 + 32);
+        const int gw0 = (int)q_base + qrow0 + 128 * g + 32 * qg;
+        // the wave's 32 queries meet the wave's 32 MB rows: -32 < gw0 - gt0 < 32 MB
+        const bool masked = rmask || (unsigned)(gw0 - gt0 + 31) < (unsigned)(32 * MB + 31);
         LDS_AS int *bk = bk0 + g * NB * 64, *bi = bi0 + g * NB * 64;
         // pairs of m-blocks = 32 candidates a lane, lower rows first (the
         // stable tie order across pairs; inside one, v orders by row)
@@ -679,8 +714,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
         rdA(0, 0, acur);
         if constexpr (PF2) rdA(0, 1, anxt);
         stage();
-        if constexpr (PF2) s_rs = i8_rsrc(s_row);   // the prologue's stages moved the cursor
-        int x = 0;
+        if constexpr (PF2 || ONE) s_rs = i8_rsrc(s_row);   // the prologue's stages moved the cursor
+        if constexpr (ONE) {
+            s_slot = s_x % NST;
+            s_nslot = s_t % NNR;
+        }
+        int x = 0, xs = 0;   // xs = x % NST (ONE)
         e_b = i8_blk_of(tab, t_lo);
         e_t0 = i8_rfl(tab->t0[e_b]);
         e_t1 = i8_rfl(tab->t0[e_b + 1]);
@@ -768,7 +807,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                 for (int ks = 0; ks < 4; ks++) {
                     if (ks < kt) {
                         if (ks + 1 < kt) {
-                            rdA(x, ks + 1, anxt);
+                            rdA(ONE ? xs : x, ks + 1, anxt);
                             // keep the reads ahead of this K-step's MFMAs:
                             // left alone, the scheduler sinks them behind the
                             // MFMAs into the same registers, and each MFMA
@@ -777,11 +816,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                         } else if (x + 1 < total) {
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x + 1)
-                            rdA(x + 1, 0, anxt);
+                            rdA(ONE ? (xs == NST - 1 ? 0 : xs + 1) : x + 1, 0, anxt);
                             // the next tile's norms arrived with its first
                             // chunk: its init words load under this K-step's
                             // MFMAs and the epilogue
-                            stage();
+                            if constexpr (ONE) stage1();
+                            else stage();
                         }
                         // (QG = 2: the first K-step of group 1 takes
                         // group 0's init words as its C operand)
@@ -798,6 +838,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                     }
                 }
                 x++;
+                if constexpr (ONE) xs = xs == NST - 1 ? 0 : xs + 1;
             }
             epilogue(t, acc, x);
         }
@@ -1029,7 +1070,7 @@ extern "C" int knn_launch_dist_i8(int kp, int kl, int lpq, int k, const void *qs
         else if (nks <= 4) launch_i8<KNN_I8_KL_S, 4, 4, 2, 8, 5, 2>(I8_ARGS);
         else if (nks <= 8) launch_i8<KNN_I8_KL_S, 8, 4, 2, 8, 5, 2>(I8_ARGS);
         else if (nks <= 16) launch_i8<KNN_I8_KL_S, 16, 4, 2, 8, 5, 2>(I8_ARGS);
-        else if (nks <= 25) launch_i8<KNN_I8_KL_S, 25, 4, 2, 7, 5, 2>(I8_ARGS);   // one-tile ring (SSLOT)
+        else if (nks <= 25) launch_i8<KNN_I8_KL_S, 25, 4, 2, 7, 6, 2>(I8_ARGS);   // one-tile ring (SSLOT); 6-entry buffers (r06_s32)
         else launch_i8<KNN_I8_KL_S, 28, 4, 2, 8, 5, 2>(I8_ARGS);
     } else if (kl == KNN_I8_KL_S) {
         // 12-entry lists merge cheaply: 5-entry buffers (merging sooner)
