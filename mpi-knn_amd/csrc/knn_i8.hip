@@ -700,10 +700,12 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
     // PF2 (half-tile kernel, long rows): A fragments are read two K-steps
     // ahead instead of one, so a read has four MFMAs (two of this wave's
     // K-steps) to land under instead of two.  Barrier B(y) then sits two
-    // K-steps before chunk y's first one; every read of chunk y - 1 was
-    // issued before it, and the lgkmcnt(0) ahead of the barrier has seen
-    // them complete, so the stage issued after B(y) may overwrite chunk y -
-    // 1's slot (as with one-deep reads, whose B(y) sits a K-step later).
+    // K-steps before chunk y's first one, and the stage issued after it
+    // overwrites chunk y - 2's slot (z = y + NST - 2).  The reads still in
+    // flight there are those of the two K-steps before chunk y: both in
+    // chunk y - 1 unless it has a single K-step (a tile's last chunk at 25
+    // K-steps), when the older one is chunk y - 2's last -- only that
+    // barrier waits for them (lgkmcnt(0)) before the stage.
     // (PF2 is defined with the bounds above: 28 K-steps spill)
     if (total > 0) {
 #pragma unroll
@@ -762,7 +764,7 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                     const int fn = f + 2;
                     if (fn < NKS) {
                         if ((fn & 3) == 0) {
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            // (chunk y - 1 is a whole chunk of 4 K-steps here)
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x0 + fn / 4)
                             rdA(SSLOT ? (fn >> 2) : x0 + (fn >> 2), 0, anx2);
@@ -773,7 +775,9 @@ __global__ __launch_bounds__(64 * W, WPS) void k_dist_topk_i8(
                         }
                     } else if (more) {
                         if (fn == NKS) {
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            // a one-K-step last chunk: K-step NKS - 2's read
+                            // (chunk y - 2's last) may still be in flight
+                            if constexpr ((NKS & 3) == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                             wait_next();
                             __builtin_amdgcn_s_barrier();   // B(x0 + NCH)
                             rdA(SSLOT ? 0 : x0 + NCH, 0, anx2);
