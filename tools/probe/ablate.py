@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Ablated copies of k_dist_topk_i8 for kbench8 (diagnostic; the product
-source carries no hooks).  Each variant is the product file with textual
+source carries no hooks).  The patches target the one-deep chunk loop;
+since round 6 the 8..25-K-step half-tile kernels (MNIST) run the two-deep
+PF2 loop, which these patterns do not touch -- re-derive them before
+ablating an MNIST-shaped launch.  Each variant is the product file with textual
 patches applied, compiled into tools/probe/abl/libkbench8_<name>.so; time it
 with  KB8_SO=tools/probe/abl/libkbench8_<name>.so python tools/probe/kbench8.py
 
