@@ -54,8 +54,9 @@
  *                         group's timeout)
  *   KNN_RING_LOOPBACK=1   P virtual ranks on device 0 (tests)
  *   KNN_NO_SHADOW_RING=1  ring moves element blocks, not shadow/byte blocks
- *   KNN_XCD_ORDER=1       distance launches in the XCD-grouped workgroup
- *                         order instead of split-major
+ *   KNN_XCD_ORDER=1 / 0   distance launches in the XCD-grouped / the
+ *                         split-major workgroup order (unset: XCD-grouped
+ *                         for split-filter launches of <= 2 splits)
  *   KNN_MAT / KNN_MPI_COMPAT  the CLIs: .mat path, bug-compatible mode
  *   (mpiknn/ring.py: KNN_NO_S8=1 packs element blocks, not the byte block
  *   of knn_block_pack_s8)

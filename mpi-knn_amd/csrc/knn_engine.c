@@ -35,7 +35,7 @@ struct knn_ctx {
     size_t nq, nq_pad, n, block_cap;
     int k;
     int kp, kl;         /* state capacity / per-lane list length serving k */
-    int xord;           /* k_dist_topk workgroup order (0 split-major, 1 XCD-grouped) */
+    int xord;           /* workgroup order: 0 split-major, 1 XCD-grouped, -1 by the launch (xord_for) */
     int h16;            /* this search's contraction runs on fp16 MFMA (exact) */
     int i8;             /* ... on int8 MFMA over byte blocks (knn_i8.hip, exact) */
     int shadow;         /* step_shadow form: 0 none, 1 fp16 shadow rows, 2 byte blocks */
@@ -482,7 +482,16 @@ int knn_ctx_create_dt(knn_ctx_t **out, int device, size_t nq, size_t n, size_t b
     c->kl = knn_kl_for(c->kp, dtype);
     c->lpq = 4;
     c->klx = c->kl;
-    c->xord = getenv("KNN_XCD_ORDER") && getenv("KNN_XCD_ORDER")[0] == '1';   /* split-major by default (the XCD-grouped order measured no faster) */
+    /* workgroup order: KNN_XCD_ORDER=1 / 0 forces the XCD-grouped / the
+     * split-major order; unset (-1), split-filter launches of <= 2 splits
+     * take the XCD-grouped one -- a query block's splits side by side on one
+     * XCD share its query rows there (gist, 2 splits: 1419 -> 1399 ms a
+     * launch), while at more splits it costs the corpus tiles' sharing
+     * (mnist-real, 6 splits: 16.97 -> 19.99 ms) */
+    {
+        const char *xe = getenv("KNN_XCD_ORDER");
+        c->xord = xe && xe[0] == '1' ? 1 : (xe && xe[0] == '0' ? 0 : -1);
+    }
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
 
     const size_t np = c->nq_pad;
@@ -870,6 +879,12 @@ static int split_cache_put(knn_ctx_t *c, size_t nc, int best)
     c->split_cache[e].klx = c->klx;
     c->split_cache[e].best = best;
     return best;
+}
+
+/* the distance launch's workgroup order (c->xord, -1 = by the launch) */
+static int xord_for(const knn_ctx_t *c, int nsplit)
+{
+    return c->xord >= 0 ? c->xord : (c->split && nsplit <= 2);
 }
 
 /* Corpus splits per query block: the count with the smallest modelled
@@ -1360,7 +1375,7 @@ static int ctx_step_impl(knn_ctx_t *c, const void *d_cblock, const void *d_sbloc
                                   cblk, knn_rows_pad(c->block_cap), c_base, (int)nc, (int)c->n, c->meta,
                                   nsplit, c->part_d[set], c->part_i[set], c->part_T[set], (int)c->nq_pad,
                                   c->qthr, c->split ? c->qsp : c->qsh, csh, cn_ptr,
-                                  (c->xord ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0) |
+                                  (xord_for(c, nsplit) ? KNN_DIST_XORD : 0) | (c->h16 ? KNN_DIST_H16 : 0) |
                                       (c->shadow ? KNN_DIST_SHADOW : 0) | (c->split ? KNN_DIST_SPLIT : 0),
                                   c->split ? (float)(-2.0 / ((double)c->sscale * c->sscale)) : -2.f, ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
@@ -1532,7 +1547,7 @@ static int ctx_step_split_n(knn_ctx_t *c, int nblk, const void *const *d_cblocks
     }
     RCHK(knn_launch_dist_split_n(c->dtype, c->kp, c->k, c->qblk, c->q_rows_pad, c->q_base, (int)c->nq, c->qsp, &tab,
                                  (int)c->n, c->meta, nsplit, c->part_d[set], c->part_i[set], c->part_T[set],
-                                 (int)c->nq_pad, c->qthr, c->xord, (float)(-2.0 / ((double)c->sscale * c->sscale)),
+                                 (int)c->nq_pad, c->qthr, xord_for(c, nsplit), (float)(-2.0 / ((double)c->sscale * c->sscale)),
                                  ds));
     if (ev) HIPCHK(hipEventRecord(ev[1], ds));
     HIPCHK(hipEventRecord(c->ev_ds[set], ds));
